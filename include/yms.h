@@ -1,0 +1,182 @@
+/* yms.h -- C-ABI of the MI355X-native YOLO-MS / YOLOv8 detector hot path.
+ *
+ * Plain C, no torch types: raw device pointers, sizes and a hipStream_t passed as void*.
+ * Every call is stream-ordered and asynchronous, allocates nothing (caller-owned outputs
+ * and workspaces), is thread-compatible, and returns a status instead of throwing.
+ *
+ * Activation layout: NHWC.  A "view" of an activation is (ptr, ld, off): element
+ * (n, y, x, c) lives at ptr[((n*H + y)*W + x)*ld + off + c].  ld and off are multiples of 8
+ * elements; channels in [C, round_up(C,8)) of a buffer are kept zero by the producers.
+ * dtype: YMS_F32 / YMS_BF16 / YMS_F16 for activations and packed weights; every
+ * accumulation, BN statistic and parameter gradient is fp32.
+ *
+ * Reference interfaces each entry point replaces (paths relative to the reference repo
+ * rafaelghiorzi/YOLO-MS):
+ *   yms_conv_fwd            components.py:69-77 Conv.forward (Conv2d->BN->SiLU), the
+ *                           Bottleneck residual add (:87-93), the C2f/SPPF/neck/head torch.cat
+ *                           (:119, :146, yolov8_neck.py:79-91, yolov8_head.py:122) via y_off,
+ *                           and the head's biased 1x1 nn.Conv2d (yolov8_head.py:86-109)
+ *   yms_conv_dgrad/_wgrad   autograd of the above (train.py:371 loss.backward())
+ *   yms_bn_*                components.py:73 nn.BatchNorm2d(eps=1e-3, momentum=0.03), train+eval
+ *   yms_sppf_pool_*         components.py:136-146 three chained MaxPool2d(5,1,2)
+ *   yms_upsample2x_*        components.py:153-160 Upsample (nearest x2)
+ *   yms_head_decode         yolov8_head.py:127-158 make_anchors + DFL (components.py:162-191)
+ *   yms_nms_*               train.py:63-113 / tools/test.py:166-218 post-process and the
+ *                           torchvision.ops.nms(boxes, scores, iou) call at train.py:93
+ */
+#ifndef YMS_H
+#define YMS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int yms_status;
+#define YMS_OK 0
+#define YMS_ERR_INVALID 1
+#define YMS_ERR_UNSUPPORTED 2
+#define YMS_ERR_LAUNCH 3
+
+#define YMS_F32 0
+#define YMS_BF16 1
+#define YMS_F16 2
+
+#define YMS_ACT_NONE 0
+#define YMS_ACT_SILU 1
+
+/* One convolution: input [n, h, w, cin] -> output [n, ho, wo, cout], square kernel k,
+ * stride, pad (ho = (h + 2*pad - k)/stride + 1). */
+typedef struct {
+  int n, h, w, cin, cout, k, stride, pad, ho, wo, dtype;
+} yms_conv_shape;
+
+const char* yms_version(void);
+const char* yms_status_string(yms_status s);
+
+/* ---- weights ------------------------------------------------------------------------ */
+/* Elements of the packed weight for the forward / dgrad GEMM (16-bit or fp32 per dtype). */
+size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad);
+/* w: fp32 [cout][cin][k][k] (nn.Conv2d layout) -> packed dtype layout.
+ * for_dgrad = 0: [cout_pad][K] with K = (kh, kw, cin_pad8) chunk order;
+ * for_dgrad = 1: [cin_pad][K'] with K' = (kh, kw, cout_pad8). */
+yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* packed,
+                                int for_dgrad, void* stream);
+
+/* ---- convolution (implicit GEMM on MFMA) --------------------------------------------- */
+/* Number of fp32 rows of BN partial statistics written by yms_conv_fwd(stats != NULL);
+ * the stats workspace is [rows][2][stats_ld] floats, stats_ld = yms_conv_stats_ld(). */
+int yms_conv_stats_rows(const yms_conv_shape* s);
+int yms_conv_stats_ld(const yms_conv_shape* s);
+/* Forward.  stats == NULL: y = act(conv(x)*scale[c] + shift[c]) (+ res) (scale/shift may
+ * be NULL = identity).  stats != NULL (training): y = conv(x) (pre-BN z) and per-tile
+ * partial sums (sum z, sum z^2) into stats. */
+yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
+                        const void* wpacked, void* y, int y_ld, int y_off,
+                        const float* scale, const float* shift, int act,
+                        const void* res, int res_ld, int res_off, float* stats, void* stream);
+/* dx (+)= conv_transpose(dz, W) with wpacked_t = yms_conv_pack_weight(.., for_dgrad=1). */
+yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
+                          const void* wpacked_t, void* dx, int dx_ld, int dx_off,
+                          int accumulate, void* stream);
+/* dw[cout][cin][k][k] (+)= sum_pixels x (*) dz, fp32; ws = split-K partial slabs. */
+size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s);
+yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
+                          const void* dz, int dz_ld, int dz_off, float* ws, size_t ws_bytes,
+                          float* dw, int accumulate, void* stream);
+
+/* ---- batch norm + activation ---------------------------------------------------------- */
+/* Eval: scale = g/sqrt(rv+eps), shift = b - rm*scale (bias-only conv: g=NULL -> scale 1, shift b). */
+yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float* rmean,
+                       const float* rvar, float eps, float* scale, float* shift, void* stream);
+/* Train: reduce partial stats of `count` pixels -> mean/invstd, scale/shift, and update the
+ * running buffers (unbiased var, momentum) exactly like nn.BatchNorm2d.  mean_invstd: [2][c]. */
+yms_status yms_bn_finalize(int c, const float* stats, int rows, int stats_ld, long count,
+                           const float* gamma, const float* beta, float* rmean, float* rvar,
+                           float momentum, float eps, float* mean_invstd, float* scale,
+                           float* shift, void* stream);
+/* y = act(z*scale + shift) (+ res), over npix pixels x c channels. */
+yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                          const float* scale, const float* shift, int act,
+                          const void* res, int res_ld, int res_off,
+                          void* y, int y_ld, int y_off, void* stream);
+/* Backward of y = silu(bn(z)) (+res):
+ *   reduce: partial sums of da and da*xhat (da = gy * silu'(a), a = z*scale+shift) -> ws
+ *   finalize: dgamma, dbeta (+=) and the two per-channel coefficients
+ *   apply: dz = scale*(da - mean(da) - xhat*mean(da*xhat)), written over dz (may alias z);
+ *          gres (+)= gy when gres != NULL (residual branch). */
+int yms_bn_bwd_rows(long npix);
+yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                                 const void* gy, int gy_ld, int gy_off, const float* scale,
+                                 const float* shift, const float* mean_invstd, int act,
+                                 float* ws, void* stream);
+yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count,
+                                   float* dgamma, float* dbeta, float* coef, void* stream);
+yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                                const void* gy, int gy_ld, int gy_off, const float* scale,
+                                const float* shift, const float* mean_invstd, const float* coef,
+                                int act, void* dz, int dz_ld, int dz_off,
+                                void* gres, int gres_ld, int gres_off, void* stream);
+/* Bias-only backward of the head's 1x1 nn.Conv2d: dbias (+)= sum over pixels of gy. */
+yms_status yms_bias_bwd(int dtype, long npix, int c, const void* gy, int gy_ld, int gy_off,
+                        float* ws, float* dbias, void* stream);
+
+/* ---- SPPF pools / upsample / layout ---------------------------------------------------- */
+/* buf holds 4 consecutive channel slots of width c at channel offset off: slot0 = input x,
+ * slots 1..3 <- maxpool5 applied 1,2,3 times (= clipped 5x5 / 9x9 / 13x13 window max). */
+yms_status yms_sppf_pool_fwd(int dtype, int n, int h, int w, int c, void* buf, int ld, int off,
+                             void* stream);
+/* gbuf: grads of the 4 slots; accumulates slot3->slot2->slot1->slot0 through the cascaded
+ * pools with PyTorch's first-max argmax (slots 1..2 grads are modified in place). */
+size_t yms_sppf_ws_bytes(int n, int h, int w, int c);
+yms_status yms_sppf_pool_bwd(int dtype, int n, int h, int w, int c, const void* buf, int ld,
+                             int off, void* gbuf, int gld, int goff, void* ws, void* stream);
+yms_status yms_upsample2x_fwd(int dtype, int n, int h, int w, int c, const void* x, int x_ld,
+                              int x_off, void* y, int y_ld, int y_off, void* stream);
+yms_status yms_upsample2x_bwd(int dtype, int n, int h, int w, int c, const void* gy, int gy_ld,
+                              int gy_off, void* gx, int gx_ld, int gx_off, int accumulate,
+                              void* stream);
+/* NCHW fp32 images -> NHWC dtype, channels padded with zeros up to ld. */
+yms_status yms_pack_input(int dtype, int n, int c, int h, int w, const float* x, void* y, int ld,
+                          void* stream);
+/* NHWC view (dtype) <-> NCHW contiguous (dtype_nchw: YMS_F32/BF16/F16). */
+yms_status yms_nhwc_to_nchw(int dtype, int dtype_nchw, int n, int h, int w, int c, const void* x,
+                            int ld, int off, void* y, void* stream);
+yms_status yms_nchw_to_nhwc(int dtype_nchw, int dtype, int n, int h, int w, int c, const void* x,
+                            void* y, int ld, int off, int accumulate, void* stream);
+/* hipMemsetAsync(p, 0, bytes) on the stream. */
+yms_status yms_zero(void* p, size_t bytes, void* stream);
+/* y = cast(x) elementwise (fp32 <-> dtype), count elements. */
+yms_status yms_cast(int dtype_in, int dtype_out, long count, const void* x, void* y, void* stream);
+
+/* ---- head decode + NMS ------------------------------------------------------------------- */
+/* Raw head maps lvl[i]: NHWC [n, h_i, w_i, no_ld] with channels (64 DFL box logits, nc cls
+ * logits).  out: [n, A, 4+nc] fp32 = (cx, cy, w, h)*stride_i, sigmoid(cls).  When nms_score
+ * is not NULL the NMS prep is fused: boxes_xyxy [n,A,4], score [n,A], label [n,A] (-1 when
+ * score <= conf). */
+yms_status yms_head_decode(int dtype, int n, int nc, int nlev, const void* const* lvl,
+                           const int* hs, const int* ws, int no_ld, const float* strides,
+                           float* out, float conf, float* boxes_xyxy, float* nms_score,
+                           int* label, void* stream);
+/* Standalone DFL integral: x [n][4*ch][A] (dtype) -> out [n][4][A] = sum_j j*softmax_j. */
+yms_status yms_dfl(int dtype, int n, int A, int ch, const void* x, void* out, void* stream);
+/* Same prep from an already-decoded [n, A, 4+nc] fp32 tensor. */
+yms_status yms_nms_prep(int n, int A, int nc, const float* pred, float conf, float* boxes_xyxy,
+                        float* score, int* label, void* stream);
+/* Class-wise NMS over the prep output.  keep_idx[n][A] (anchor ids), keep_lbl[n][A],
+ * counts[n]; per image the kept rows are ordered by class ascending, then by descending
+ * score (ties by anchor id), exactly like the reference's per-class torchvision loop. */
+size_t yms_nms_ws_bytes(int n, int A, int nc);
+yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, const float* score,
+                             const int* label, double iou, int64_t* keep_idx, int* keep_lbl,
+                             int* counts, void* ws, size_t ws_bytes, void* stream);
+/* Plain torchvision.ops.nms(boxes[m,4], scores[m], iou) on one set -> keep[m], *count. */
+yms_status yms_nms_single(int m, const float* boxes, const float* scores, double iou,
+                          int64_t* keep, int* count, void* ws, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* YMS_H */

@@ -1,0 +1,63 @@
+"""Test helpers: drive single C-ABI ops of libyms.so on torch tensors (test infra only)."""
+import ctypes
+
+import torch
+import torch.nn.functional as F
+
+from yms import _lib as L
+
+DT = {"f32": torch.float32, "bf16": torch.bfloat16, "f16": torch.float16}
+
+
+def r8(c):
+    return (c + 7) // 8 * 8
+
+
+def nhwc(x, dtype, ld=None, off=0):
+    """NCHW fp32 -> zero-padded NHWC [n,h,w,ld] buffer of dtype with x at channel offset off."""
+    n, c, h, w = x.shape
+    ld = ld or r8(off + c)
+    buf = torch.zeros((n, h, w, ld), dtype=dtype, device="cuda")
+    buf[..., off:off + c] = x.permute(0, 2, 3, 1).to(dtype)
+    return buf
+
+
+def nchw(buf, c, off=0):
+    return buf[..., off:off + c].permute(0, 3, 1, 2).float()
+
+
+def shape(n, h, w, cin, cout, k, s, dtype):
+    p = k // 2
+    ho, wo = (h + 2 * p - k) // s + 1, (w + 2 * p - k) // s + 1
+    return L.ConvShape(n, h, w, cin, cout, k, s, p, ho, wo, L.dtype_code(dtype))
+
+
+def pack(w, sh, dtype, for_dgrad):
+    sp = ctypes.pointer(sh)
+    out = torch.empty(L.lib().yms_conv_packed_elems(sp, for_dgrad), dtype=dtype, device="cuda")
+    wc = w.float().contiguous().cuda()
+    L.call("yms_conv_pack_weight", sp, wc.data_ptr(), out.data_ptr(), for_dgrad, L.stream_ptr())
+    return out
+
+
+def conv_fwd(xb, w, sh, dtype, scale=None, shift=None, act=0, res=None, stats=False, yld=None, yoff=0,
+             xoff=0):
+    sp = ctypes.pointer(sh)
+    wp = pack(w, sh, dtype, 0)
+    yld = yld or r8(yoff + sh.cout)
+    y = torch.zeros((sh.n, sh.ho, sh.wo, yld), dtype=dtype, device="cuda")
+    st = None
+    if stats:
+        rows, ld = L.lib().yms_conv_stats_rows(sp), L.lib().yms_conv_stats_ld(sp)
+        st = torch.zeros((rows, 2, ld), dtype=torch.float32, device="cuda")
+    L.call("yms_conv_fwd", sp, xb.data_ptr(), xb.shape[-1], xoff, wp.data_ptr(), y.data_ptr(), yld, yoff,
+           L.ptr(scale), L.ptr(shift), act, L.ptr(res), res.shape[-1] if res is not None else 0, 0,
+           L.ptr(st), L.stream_ptr())
+    return y, st
+
+
+def ref_conv(x, w, s, dtype):
+    """fp32 conv on operands rounded to `dtype` (what the MFMA path multiplies)."""
+    xr = x.to(dtype).float()
+    wr = w.to(dtype).float()
+    return F.conv2d(xr, wr, None, s, w.shape[-1] // 2)

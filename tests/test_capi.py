@@ -1,0 +1,89 @@
+"""CPU tier: the C-ABI library builds/loads and exports every function include/yms.h declares;
+host-side helpers (shape checks, workspace sizing, plan construction) work without a GPU."""
+import ctypes
+import os
+import re
+
+import pytest
+import torch
+
+from yms import _lib as L
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def header_functions():
+    txt = open(os.path.join(ROOT, "include", "yms.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[a-z_0-9]+\**\s+\**(yms_[a-z_0-9]+)\s*\(", txt, flags=re.M)))
+
+
+def test_header_symbols_exported():
+    names = header_functions()
+    assert len(names) >= 30
+    lib = ctypes.CDLL(L.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+    # every declared function is also bound (with argtypes) by the Python layer
+    assert set(names) <= set(L.EXPORTED), set(names) - set(L.EXPORTED)
+
+
+def test_version_and_status():
+    assert b"gfx950" in L.lib().yms_version()
+    assert L.lib().yms_status_string(1) == b"invalid argument"
+
+
+def test_host_shape_validation_and_sizes():
+    sh = L.ConvShape(2, 64, 64, 32, 64, 3, 2, 1, 32, 32, L.BF16)
+    sp = ctypes.pointer(sh)
+    # packed weights: cout padded to 128 rows, K = 9 taps x 32 ch padded to 32-element tiles
+    assert L.lib().yms_conv_packed_elems(sp, 0) == 128 * 9 * 32
+    assert L.lib().yms_conv_stats_ld(sp) == 128
+    assert L.lib().yms_conv_stats_rows(sp) > 0
+    assert L.lib().yms_conv_wgrad_ws_bytes(sp) > 0
+    bad = L.ConvShape(2, 64, 64, 32, 64, 3, 2, 1, 31, 32, L.BF16)
+    assert L.lib().yms_conv_packed_elems(ctypes.pointer(bad), 0) == 0
+    assert L.lib().yms_conv_fwd(ctypes.pointer(bad), None, 8, 0, None, None, 8, 0, None, None, 0, None, 0, 0,
+                                None, None) == 1
+    assert L.lib().yms_nms_ws_bytes(32, 8400, 80) > 32 * 8400 * 28
+
+
+def test_null_pointers_rejected_without_gpu():
+    sh = L.ConvShape(1, 8, 8, 8, 8, 3, 1, 1, 8, 8, L.F32)
+    assert L.lib().yms_conv_fwd(ctypes.pointer(sh), None, 8, 0, None, None, 8, 0, None, None, 0, None, 0, 0,
+                                None, None) == 1
+    assert L.lib().yms_affine_act(L.BF16, 10, 8, None, 8, 0, None, None, 0, None, 0, 0, None, 8, 0, None) == 1
+    assert L.lib().yms_nms_classwise(1, 10, 1, None, None, None, 0.5, None, None, None, None, 0, None) == 1
+
+
+def test_plan_construction_s640():
+    from yms import runner
+    from yolov8.yolov8 import YOLOv8
+    m = YOLOv8("s", 80)
+    x = torch.empty(4, 3, 640, 640, device="meta")
+    for tr in (False, True):
+        m.train(tr)
+        p = runner.get_plan(m, [x], torch.bfloat16, tr)
+        assert abs(p.flops / 4 / 1e9 - 25.79) < 0.01
+        assert len(p.ops) == 66
+    with pytest.raises(RuntimeError, match="multiple of 32"):
+        runner.get_plan(m, [torch.empty(1, 3, 100, 100, device="meta")], torch.float32, False)
+
+
+def test_state_dict_keys_identical_to_reference():
+    import json
+    from yolov8.yolov8 import YOLOv8
+    ref = json.load(open(os.path.join(ROOT, "tests", "golden", "state_keys.json")))
+    for tag in ("n_80", "s_80", "l_80", "n_1"):
+        v, nc = tag.split("_")
+        m = YOLOv8(v, int(nc))
+        assert [[k, list(t.shape)] for k, t in m.state_dict().items()] == ref[tag], tag
+    from yolov8.model.components import yolo_params
+    with pytest.raises(ValueError, match="Unknown YOLOv8 version: xs"):
+        yolo_params("xs")
+
+
+def test_cpu_input_raises():
+    from yolov8.model.components import Conv
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        Conv(3, 8)(torch.zeros(1, 3, 8, 8))

@@ -1,0 +1,129 @@
+"""GPU parity of the implicit-GEMM convolution kernels (forward with every epilogue,
+dgrad, wgrad) against fp32 PyTorch-CPU convolution on the same dtype-rounded operands."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from hiputil import DT, conv_fwd, nchw, nhwc, pack, r8, ref_conv, shape
+from yms import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+# (n, cin, h, w, cout, k, stride): stem, odd sizes, padded channels, wide outputs, 1x1
+SHAPES = [
+    (2, 3, 13, 10, 16, 3, 2),
+    (2, 16, 9, 7, 24, 1, 1),
+    (1, 64, 20, 20, 80, 3, 1),
+    (2, 32, 40, 40, 64, 3, 2),
+    (1, 256, 10, 10, 512, 1, 1),
+    (3, 8, 17, 19, 130, 3, 1),
+    (1, 1, 8, 8, 1, 3, 1),
+    (2, 80, 11, 12, 80, 1, 1),
+]
+# bf16/f16 outputs are rounded to 8/11 significant bits; fp32 uses the exact-f32 MFMA
+TOL = {"f32": 2e-5, "bf16": 1e-2, "f16": 2e-3}
+
+
+def _close(got, ref, tol):
+    scale = ref.abs().max().item() + 1e-6
+    err = (got - ref).abs().max().item()
+    assert err <= tol * scale + 1e-6, f"max err {err:.3g} vs scale {scale:.3g} (tol {tol})"
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16", "f16"])
+@pytest.mark.parametrize("shp", SHAPES)
+def test_conv_fwd_affine_silu_residual(shp, dt):
+    n, cin, h, w, cout, k, s = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(hash(shp) % 1000)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh_ = torch.randn(cout, generator=g) * 0.1
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    res = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+    y, _ = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, sc.cuda(), sh_.cuda(), L.ACT_SILU, nhwc(res, dtype))
+    z = ref_conv(x, wt, s, dtype)
+    ref = F.silu(z * sc.view(1, -1, 1, 1) + sh_.view(1, -1, 1, 1)) + res.to(dtype).float()
+    _close(nchw(y, cout).cpu(), ref, TOL[dt])
+    # padded channels of the output buffer stay zero
+    if r8(cout) != cout:
+        assert y[..., cout:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("shp", SHAPES[:6])
+def test_conv_fwd_stats(shp, dt):
+    n, cin, h, w, cout, k, s = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(7)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    y, st = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, stats=True)
+    z = ref_conv(x, wt, s, dtype)
+    _close(nchw(y, cout).cpu(), z, TOL[dt])
+    s1 = st[:, 0, :cout].double().sum(0).cpu()
+    s2 = st[:, 1, :cout].double().sum(0).cpu()
+    _close(s1.float(), z.sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
+    _close(s2.float(), (z * z).sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
+
+
+def test_conv_fwd_channel_offsets():
+    """Input read from / output written to channel slices of wider buffers (concat placement)."""
+    dtype = torch.bfloat16
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(2, 24, 9, 9, generator=g)
+    wt = torch.randn(40, 24, 3, 3, generator=g) / 15
+    xb = nhwc(x, dtype, ld=48, off=16)
+    shp_ = shape(2, 9, 9, 24, 40, 3, 1, dtype)
+    y, _ = conv_fwd(xb, wt, shp_, dtype, act=0, yld=64, yoff=8, xoff=16)
+    ref = ref_conv(x, wt, 1, dtype)
+    _close(nchw(y, 40, off=8).cpu(), ref, TOL["bf16"])
+    assert y[..., :8].abs().max().item() == 0 and y[..., 48:].abs().max().item() == 0
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("shp", SHAPES)
+def test_conv_dgrad_wgrad(shp, dt):
+    n, cin, h, w, cout, k, s = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    dz = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+    xr = x.to(dtype).float().requires_grad_(True)
+    wr = wt.to(dtype).float().requires_grad_(True)
+    F.conv2d(xr, wr, None, s, k // 2).backward(dz.to(dtype).float())
+    sp = ctypes.pointer(shp_)
+    # dgrad, accumulate onto a pre-filled buffer
+    base = torch.randn(n, cin, h, w, generator=g)
+    dx = nhwc(base, dtype)
+    wpt = pack(wt, shp_, dtype, 1)
+    dzb = nhwc(dz, dtype)
+    L.call("yms_conv_dgrad", sp, dzb.data_ptr(), dzb.shape[-1], 0, wpt.data_ptr(), dx.data_ptr(), dx.shape[-1], 0,
+           1, L.stream_ptr())
+    _close(nchw(dx, cin).cpu(), xr.grad + base.to(dtype).float(), TOL[dt] * 2)
+    # wgrad (fp32 result, split-K slabs)
+    xb = nhwc(x, dtype)
+    wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
+    ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device="cuda")
+    dw = torch.zeros(cout, cin, k, k, device="cuda")
+    L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0, ws.data_ptr(),
+           wsb, dw.data_ptr(), 0, L.stream_ptr())
+    _close(dw.cpu(), wr.grad, 1e-4 if dt == "f32" else 2e-3)
+
+
+def test_invalid_arguments_rejected():
+    sh = shape(1, 8, 8, 8, 8, 3, 1, torch.float32)
+    sh.ho = 5   # inconsistent
+    st = L.lib().yms_conv_fwd(ctypes.pointer(sh), 1, 8, 0, 1, 1, 8, 0, None, None, 0, None, 0, 0, None,
+                              L.stream_ptr())
+    assert st == 1
+    sh = shape(1, 8, 8, 8, 8, 3, 1, torch.float32)
+    st = L.lib().yms_conv_fwd(ctypes.pointer(sh), 1, 12, 0, 1, 1, 8, 0, None, None, 0, None, 0, 0, None,
+                              L.stream_ptr())
+    assert st == 1   # ld not a multiple of 8

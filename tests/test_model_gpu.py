@@ -1,0 +1,186 @@
+"""GPU parity of the module API (yolov8.*) against golden vectors produced by the
+reference model (tests/golden) and against the CPU oracle (oracle/model_ref.py)."""
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import model_ref as M
+from yolov8.model import components as C
+from yolov8.yolov8 import YOLOv8
+
+pytestmark = pytest.mark.gpu
+GOLD = os.path.join(os.path.dirname(__file__), "golden")
+DEV = "cuda"
+
+
+def _load(name):
+    return dict(np.load(os.path.join(GOLD, name)))
+
+
+def _closed_form_local(module):
+    """Same closed-form init make_golden.py used (keys local to the block)."""
+    sd = {}
+    for k, v in module.state_dict().items():
+        if k.endswith("num_batches_tracked"):
+            sd[k] = torch.zeros_like(v)
+        elif v.dim() == 4:
+            fan = v.shape[1] * v.shape[2] * v.shape[3]
+            sd[k] = M._closed_form(k, tuple(v.shape), (3.0 / fan) ** 0.5 * 1.2)
+        elif k.endswith("bn.weight"):
+            sd[k] = M._closed_form(k, tuple(v.shape), 0.25, base=1.0)
+        elif k.endswith("bn.bias"):
+            sd[k] = M._closed_form(k, tuple(v.shape), 0.2)
+        elif k.endswith("running_mean"):
+            sd[k] = M._closed_form(k, tuple(v.shape), 0.1)
+        elif k.endswith("running_var"):
+            sd[k] = M._closed_form(k, tuple(v.shape), 0.3, base=1.2)
+        else:
+            sd[k] = M._closed_form(k, tuple(v.shape), 0.5)
+    module.load_state_dict(sd)
+    return module
+
+
+def _rel(got, ref):
+    got = torch.as_tensor(got).double().cpu()
+    ref = torch.as_tensor(ref).double()
+    return ((got - ref).norm() / (ref.norm() + 1e-12)).item()
+
+
+def _maxerr(got, ref):
+    got = torch.as_tensor(got).float().cpu()
+    ref = torch.as_tensor(ref).float()
+    return ((got - ref).abs().max() / (ref.abs().max() + 1e-12)).item()
+
+
+BLOCKS = {
+    "conv1x1": lambda: C.Conv(16, 24, 1, 1, 0),
+    "conv3x3s1": lambda: C.Conv(8, 16, 3, 1, 1),
+    "conv3x3s2": lambda: C.Conv(3, 16, 3, 2, 1),
+    "conv3x3s2_c24": lambda: C.Conv(24, 32, 3, 2, 1),
+    "bottleneck": lambda: C.Bottleneck(16, 16),
+    "c2f_n1": lambda: C.C2f(32, 32, 1),
+    "c2f_n2": lambda: C.C2f(24, 48, 2),
+    "sppf": lambda: C.SPPF(32, 32),
+}
+
+
+@pytest.mark.parametrize("name", sorted(BLOCKS))
+def test_block_fp32_vs_reference_golden(name):
+    g = _load(f"block_{name}.npz")
+    m = _closed_form_local(BLOCKS[name]()).to(DEV)
+    x = torch.from_numpy(g["x"]).to(DEV)
+    m.eval()
+    y = m(x)
+    assert _maxerr(y, g["eval_y"]) < 1e-4
+    m.train()
+    xg = x.clone().requires_grad_(True)
+    y = m(xg)
+    assert _maxerr(y.detach(), g["train_y0"]) < 1e-4
+    (y.float() * torch.from_numpy(g["cot0"]).to(DEV)).sum().backward()
+    assert _rel(xg.grad, g["dx"]) < 1e-4
+    pd = dict(m.named_parameters())
+    for k in g:
+        if k.startswith("grad:"):
+            assert _rel(pd[k[5:]].grad, g[k]) < 1e-4, k
+        if k.startswith("buf:") and "running" in k:
+            assert _maxerr(dict(m.named_buffers())[k[4:]], g[k]) < 1e-5, k
+        if k.startswith("buf:") and "num_batches" in k:
+            assert int(dict(m.named_buffers())[k[4:]]) == int(g[k])
+
+
+def test_upsample_and_dfl_golden():
+    g = _load("block_upsample.npz")
+    up = C.Upsample().to(DEV)
+    y = up(torch.from_numpy(g["x"]).to(DEV))
+    assert torch.equal(y.float().cpu(), torch.from_numpy(g["y"]))
+    g = _load("block_dfl.npz")
+    y = C.DFL().to(DEV)(torch.from_numpy(g["x"]).to(DEV))
+    assert _maxerr(y, g["y"]) < 1e-5
+
+
+@pytest.mark.parametrize("fname,v,nc", [("model_n80_2x64x64.npz", "n", 80),
+                                        ("model_n80_1x128x96.npz", "n", 80),
+                                        ("model_n1_2x64x64.npz", "n", 1)])
+def test_full_model_fp32_vs_reference_golden(fname, v, nc):
+    g = _load(fname)
+    m = YOLOv8(v, nc).to(DEV)
+    m.load_state_dict(M.init_params(v, nc))
+    x = torch.from_numpy(g["x"]).to(DEV)
+    m.eval()
+    m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    y = m(x)
+    assert y.shape == g["eval_y"].shape
+    ref = torch.from_numpy(g["eval_y"])
+    assert _maxerr(y[..., :4], ref[..., :4]) < 1e-4
+    assert (y[..., 4:].cpu() - ref[..., 4:]).abs().max().item() < 1e-5
+    m.train()
+    ys = m(x)
+    loss = 0
+    for i, t in enumerate(ys):
+        assert _maxerr(t.detach(), g[f"train_y{i}"]) < 1e-4
+        loss = loss + (t * torch.from_numpy(g[f"cot{i}"]).to(DEV)).sum()
+    loss.backward()
+    pd = dict(m.named_parameters())
+    for k in g:
+        if k.startswith("gsum:"):
+            gr = pd[k[5:]].grad.double().cpu()
+            s, a = g[k]
+            assert abs(gr.abs().sum().item() - a) <= 2e-3 * abs(a) + 1e-6, k
+        elif k.startswith("grad:"):
+            assert _rel(pd[k[5:]].grad, g[k]) < 2e-4, k
+        elif k.startswith("buf:"):
+            assert _maxerr(dict(m.named_buffers())[k[4:]], g[k]) < 1e-5, k
+
+
+def test_s640_bf16_eval_against_oracle():
+    """YOLO-MS-S (= YOLOv8-s graph) 640x640 bf16 inference vs the fp32 CPU oracle."""
+    v, nc = "s", 80
+    sd = M.init_params(v, nc)
+    m = YOLOv8(v, nc).to(DEV)
+    m.load_state_dict(sd)
+    m.eval()
+    m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    x = torch.randn(2, 3, 640, 640, generator=torch.Generator().manual_seed(0))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        y = m(x.to(DEV)).cpu()
+    with torch.no_grad():
+        ref = M.forward(dict(sd), v, nc, x, False)
+    assert y.shape == (2, 8400, 84) and y.dtype == torch.float32
+    cls_err = (y[..., 4:] - ref[..., 4:]).abs().max().item()
+    box_rel = _rel(y[..., :4], ref[..., :4])
+    # bf16 end-to-end drift (CPU bf16 autocast itself drifts 4.5e-2 box / 1.9e-3 cls)
+    assert cls_err < 3e-2, cls_err
+    assert box_rel < 2e-2, box_rel
+
+
+def test_s_bf16_train_grads_against_oracle():
+    v, nc = "s", 80
+    sd = M.init_params(v, nc)
+    m = YOLOv8(v, nc).to(DEV)
+    m.load_state_dict(sd)
+    m.train()
+    x = torch.randn(2, 3, 128, 128, generator=torch.Generator().manual_seed(1))
+    with torch.autocast("cuda", dtype=torch.bfloat16):
+        outs = m(x.to(DEV))
+    loss = sum((o.float() ** 2).mean() for o in outs)
+    loss.backward()
+    p = {k: (t.clone().requires_grad_(True) if t.is_floating_point() and "running" not in k
+             and k != "head.dfl.conv.weight" else t.clone()) for k, t in sd.items()}
+    r = M.forward(p, v, nc, x, True)
+    sum((o ** 2).mean() for o in r).backward()
+    pd = dict(m.named_parameters())
+    worst = 0.0
+    for k, t in p.items():
+        if t.grad is None or k not in pd:
+            continue
+        worst = max(worst, _rel(pd[k].grad, t.grad))
+    assert worst < 0.1, worst
+
+
+def test_cpu_tensor_fails_loudly():
+    m = C.Conv(3, 8).to(DEV)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m(torch.zeros(1, 3, 8, 8))

@@ -1,0 +1,710 @@
+// BatchNorm / SiLU / residual, SPPF pooling, nearest-x2 upsample and layout kernels for the
+// YOLOv8 hot path on gfx950.  All are HBM-bound streaming kernels: 16-B vectorised NHWC
+// accesses (8 channels per item), grid-stride loops, fp32 math, deterministic reductions
+// (per-block partial rows reduced in a fixed order, fp64 final sums).
+//
+// Reference semantics (paths relative to rafaelghiorzi/YOLO-MS):
+//   nn.BatchNorm2d(eps=1e-3, momentum=0.03) + nn.SiLU   yolov8/model/components.py:72-77
+//   Bottleneck residual (always on)                     yolov8/model/components.py:87-93
+//   SPPF: three chained MaxPool2d(5, 1, 2) + cat        yolov8/model/components.py:136-146
+//   Upsample nearest x2                                 yolov8/model/components.py:159-160
+#include <algorithm>
+
+#include "yms_common.hpp"
+
+namespace yms {
+
+static inline unsigned grid_for(long items, int block = 256, long cap = 16384) {
+  long g = (items + block - 1) / block;
+  if (g < 1) g = 1;
+  return (unsigned)std::min(g, cap);
+}
+
+// ------------------------------------------------------------------------------------------
+// BN fold (eval) and finalize (train)
+// ------------------------------------------------------------------------------------------
+__global__ void bn_fold_kernel(int c, const float* g, const float* b, const float* rm,
+                               const float* rv, float eps, float* scale, float* shift) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= c) return;
+  if (!g) {  // bias-only (plain nn.Conv2d)
+    scale[i] = 1.0f;
+    shift[i] = b ? b[i] : 0.0f;
+    return;
+  }
+  const float sc = g[i] / sqrtf(rv[i] + eps);
+  scale[i] = sc;
+  shift[i] = b[i] - rm[i] * sc;
+}
+
+// stats: [rows][2][ld]; 32 channels x 8 row-lanes per block, fp64 accumulation.
+__global__ void bn_finalize_kernel(int c, const float* stats, int rows, int ld, long count,
+                                   const float* g, const float* b, float* rm, float* rv,
+                                   float momentum, float eps, float* mi, float* scale,
+                                   float* shift) {
+  __shared__ double red[2][8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int ch = blockIdx.x * 32 + tx;
+  double s1 = 0.0, s2 = 0.0;
+  if (ch < c) {
+    for (int r = ty; r < rows; r += 8) {
+      s1 += stats[(long)r * 2 * ld + ch];
+      s2 += stats[(long)r * 2 * ld + ld + ch];
+    }
+  }
+  red[0][ty][tx] = s1;
+  red[1][ty][tx] = s2;
+  __syncthreads();
+  if (ty == 0 && ch < c) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < 8; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
+    const double mean = t1 / (double)count;
+    double var = t2 / (double)count - mean * mean;
+    if (var < 0.0) var = 0.0;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const double uvar = count > 1 ? var * (double)count / (double)(count - 1) : var;
+    if (rm) rm[ch] = (float)((1.0 - momentum) * (double)rm[ch] + momentum * mean);
+    if (rv) rv[ch] = (float)((1.0 - momentum) * (double)rv[ch] + momentum * uvar);
+    mi[ch] = (float)mean;
+    mi[c + ch] = invstd;
+    const float sc = g[ch] * invstd;
+    scale[ch] = sc;
+    shift[ch] = b[ch] - (float)mean * sc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// y = act(z*scale + shift) (+ res)
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void affine_act_kernel(long npix, int c, const T* z, int z_ld, int z_off,
+                                  const float* scale, const float* shift, int act, const T* res,
+                                  int res_ld, int res_off, T* y, int y_ld, int y_off) {
+  const int G = (c + 7) >> 3;
+  const long total = npix * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long pix = t / G;
+    const int g = (int)(t - pix * G);
+    const int c0 = g * 8, nv = min(8, c - c0);
+    float v[8], r[8];
+    load8(z + pix * z_ld + z_off + c0, nv, v);
+    if (res) load8(res + pix * res_ld + res_off + c0, nv, r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = min(c0 + i, c - 1);
+      float a = v[i] * (scale ? scale[ch] : 1.0f) + (shift ? shift[ch] : 0.0f);
+      if (act == YMS_ACT_SILU) a = silu_f(a);
+      if (res) a += r[i];
+      v[i] = a;
+    }
+    store8(y + pix * y_ld + y_off + c0, nv, v);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// BN + SiLU backward.  Block = 32 channel-group lanes x 8 pixel lanes; each block owns a
+// contiguous pixel range and writes one partial row [2][c] (deterministic).
+// ------------------------------------------------------------------------------------------
+constexpr int BWD_NG = 4;   // channel groups (of 8) per thread lane -> up to 1024 channels
+
+template <typename T, bool HAS_Z>
+__global__ void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld, int z_off,
+                                     const T* gy, int gy_ld, int gy_off, const float* scale,
+                                     const float* shift, const float* mi, int act, float* ws,
+                                     long pix_per_block) {
+  __shared__ float red[8][2][256 + 8];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int G = (c + 7) >> 3;
+  const long p0 = blockIdx.x * pix_per_block;
+  const long p1 = min(npix, p0 + pix_per_block);
+  for (int gbase = 0; gbase < G; gbase += 32 * BWD_NG) {
+    float acc1[BWD_NG][8], acc2[BWD_NG][8];
+#pragma unroll
+    for (int k = 0; k < BWD_NG; ++k)
+#pragma unroll
+      for (int i = 0; i < 8; ++i) { acc1[k][i] = 0.f; acc2[k][i] = 0.f; }
+    for (long pix = p0 + ty; pix < p1; pix += 8) {
+#pragma unroll
+      for (int k = 0; k < BWD_NG; ++k) {
+        const int g = gbase + tx + 32 * k;
+        if (g >= G) continue;
+        const int c0 = g * 8, nv = min(8, c - c0);
+        float gv[8], zv[8];
+        load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
+        if (HAS_Z) load8(z + pix * z_ld + z_off + c0, nv, zv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int ch = min(c0 + i, c - 1);
+          float da = gv[i], xh = 0.f;
+          if (HAS_Z) {
+            const float a = zv[i] * scale[ch] + shift[ch];
+            if (act == YMS_ACT_SILU) {
+              const float s = sigmoid_f(a);
+              da = gv[i] * (s * (1.0f + a * (1.0f - s)));
+            }
+            xh = (zv[i] - mi[ch]) * mi[c + ch];
+          }
+          acc1[k][i] += da;
+          acc2[k][i] += da * xh;
+        }
+      }
+    }
+    // reduce over the 8 pixel lanes (fixed order), one channel-group chunk at a time
+#pragma unroll
+    for (int k = 0; k < BWD_NG; ++k) {
+      const int g = gbase + tx + 32 * k;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        red[ty][0][tx * 8 + i] = acc1[k][i];
+        red[ty][1][tx * 8 + i] = acc2[k][i];
+      }
+      __syncthreads();
+      // 256 threads finalize 256 channels of this chunk
+      const int cl = threadIdx.x;  // local channel in [0, 256)
+      const int ch = (gbase + 32 * k) * 8 + cl;
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < 8; ++w) { t1 += red[w][0][cl]; t2 += red[w][1][cl]; }
+      if (ch < c) {
+        ws[(long)blockIdx.x * 2 * c + ch] = t1;
+        ws[(long)blockIdx.x * 2 * c + c + ch] = t2;
+      }
+      __syncthreads();
+      (void)g;
+    }
+  }
+}
+
+__global__ void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long count, float* dgamma,
+                                       float* dbeta, float* coef) {
+  __shared__ double red[2][8][33];
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+  const int ch = blockIdx.x * 32 + tx;
+  double s1 = 0.0, s2 = 0.0;
+  if (ch < c)
+    for (int r = ty; r < rows; r += 8) {
+      s1 += ws[(long)r * 2 * c + ch];
+      s2 += ws[(long)r * 2 * c + c + ch];
+    }
+  red[0][ty][tx] = s1;
+  red[1][ty][tx] = s2;
+  __syncthreads();
+  if (ty == 0 && ch < c) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < 8; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
+    if (dbeta) dbeta[ch] = (float)t1;
+    if (dgamma) dgamma[ch] = (float)t2;
+    if (coef) {
+      coef[ch] = (float)(t1 / (double)count);
+      coef[c + ch] = (float)(t2 / (double)count);
+    }
+  }
+}
+
+template <typename T>
+__global__ void bn_bwd_apply_kernel(long npix, int c, const T* z, int z_ld, int z_off, const T* gy,
+                                    int gy_ld, int gy_off, const float* scale, const float* shift,
+                                    const float* mi, const float* coef, int act, T* dz, int dz_ld,
+                                    int dz_off, T* gres, int gres_ld, int gres_off) {
+  const int G = (c + 7) >> 3;
+  const long total = npix * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const long pix = t / G;
+    const int g = (int)(t - pix * G);
+    const int c0 = g * 8, nv = min(8, c - c0);
+    float gv[8], zv[8], out[8];
+    load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
+    load8(z + pix * z_ld + z_off + c0, nv, zv);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int ch = min(c0 + i, c - 1);
+      const float a = zv[i] * scale[ch] + shift[ch];
+      float da = gv[i];
+      if (act == YMS_ACT_SILU) {
+        const float s = sigmoid_f(a);
+        da = gv[i] * (s * (1.0f + a * (1.0f - s)));
+      }
+      const float xh = (zv[i] - mi[ch]) * mi[c + ch];
+      out[i] = scale[ch] * (da - coef[ch] - xh * coef[c + ch]);
+    }
+    if (gres) {
+      float r[8];
+      load8(gres + pix * gres_ld + gres_off + c0, nv, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) r[i] += gv[i];
+      store8(gres + pix * gres_ld + gres_off + c0, nv, r);
+    }
+    store8(dz + pix * dz_ld + dz_off + c0, nv, out);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// SPPF pools: slot k = clipped (4k+1)x(4k+1) window max of slot 0 (== k chained MaxPool5).
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void sppf_fwd_kernel(int n, int h, int w, int c, T* buf, int ld, int off) {
+  const int G = (c + 7) >> 3;
+  const long total = (long)n * h * w * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % G);
+    long r = t / G;
+    const int x = (int)(r % w);
+    r /= w;
+    const int y = (int)(r % h);
+    const int b = (int)(r / h);
+    const int c0 = g * 8, nv = min(8, c - c0);
+    float m1[8], m2[8], m3[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { m1[i] = -INFINITY; m2[i] = -INFINITY; m3[i] = -INFINITY; }
+    for (int dy = -6; dy <= 6; ++dy) {
+      const int yy = y + dy;
+      if (yy < 0 || yy >= h) continue;
+      const int ady = dy < 0 ? -dy : dy;
+      for (int dx = -6; dx <= 6; ++dx) {
+        const int xx = x + dx;
+        if (xx < 0 || xx >= w) continue;
+        const int adx = dx < 0 ? -dx : dx;
+        const int rad = ady > adx ? ady : adx;
+        float v[8];
+        load8(buf + (((long)b * h + yy) * w + xx) * ld + off + c0, nv, v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          m3[i] = fmaxf(m3[i], v[i]);
+          if (rad <= 4) m2[i] = fmaxf(m2[i], v[i]);
+          if (rad <= 2) m1[i] = fmaxf(m1[i], v[i]);
+        }
+      }
+    }
+    T* o = buf + (((long)b * h + y) * w + x) * ld + off + c0;
+    store8(o + c, nv, m1);
+    store8(o + 2 * c, nv, m2);
+    store8(o + 3 * c, nv, m3);
+  }
+}
+
+// argmax of a 5x5 (pad 2, -inf) window over input slot `in`, PyTorch scan order, first max.
+template <typename T>
+__global__ void pool5_argmax_kernel(int n, int h, int w, int c, const T* buf, int ld, int in_off,
+                                    uint8_t* arg) {
+  const int G = (c + 7) >> 3;
+  const long total = (long)n * h * w * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % G);
+    long r = t / G;
+    const int x = (int)(r % w);
+    r /= w;
+    const int y = (int)(r % h);
+    const int b = (int)(r / h);
+    const int c0 = g * 8, nv = min(8, c - c0);
+    float best[8];
+    uint8_t idx[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; idx[i] = 255; }
+    for (int ky = 0; ky < 5; ++ky) {
+      const int yy = y - 2 + ky;
+      if (yy < 0 || yy >= h) continue;
+      for (int kx = 0; kx < 5; ++kx) {
+        const int xx = x - 2 + kx;
+        if (xx < 0 || xx >= w) continue;
+        float v[8];
+        load8(buf + (((long)b * h + yy) * w + xx) * ld + in_off + c0, nv, v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (idx[i] == 255 || v[i] > best[i] || v[i] != v[i]) {  // (val > maxval) || isnan(val)
+            best[i] = v[i];
+            idx[i] = (uint8_t)(ky * 5 + kx);
+          }
+      }
+    }
+    uint8_t* a = arg + ((((long)b * h + y) * w + x) * G + g) * 8;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) a[i] = idx[i];
+  }
+}
+
+// g[in slot] += sum over the 25 outputs o whose argmax points at this position of g[out slot]
+template <typename T>
+__global__ void pool5_gather_kernel(int n, int h, int w, int c, const uint8_t* arg, T* g, int ld,
+                                    int in_off, int out_off) {
+  const int G = (c + 7) >> 3;
+  const long total = (long)n * h * w * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int gg = (int)(t % G);
+    long r = t / G;
+    const int x = (int)(r % w);
+    r /= w;
+    const int y = (int)(r % h);
+    const int b = (int)(r / h);
+    const int c0 = gg * 8, nv = min(8, c - c0);
+    float acc[8];
+    load8(g + (((long)b * h + y) * w + x) * ld + in_off + c0, nv, acc);
+    // output o = (y - ky + 2, x - kx + 2) sees this input at window offset (ky, kx)
+    for (int ky = 0; ky < 5; ++ky) {
+      const int oy = y - ky + 2;
+      if (oy < 0 || oy >= h) continue;
+      for (int kx = 0; kx < 5; ++kx) {
+        const int ox = x - kx + 2;
+        if (ox < 0 || ox >= w) continue;
+        const long o = ((long)b * h + oy) * w + ox;
+        const uint8_t* a = arg + (o * G + gg) * 8;
+        const uint2 av = *reinterpret_cast<const uint2*>(a);
+        const uint8_t want = (uint8_t)(ky * 5 + kx);
+        float gv[8];
+        load8(g + o * ld + out_off + c0, nv, gv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const uint8_t ai = (uint8_t)(((i < 4 ? av.x : av.y) >> (8 * (i & 3))) & 0xff);
+          if (ai == want) acc[i] += gv[i];
+        }
+      }
+    }
+    store8(g + (((long)b * h + y) * w + x) * ld + in_off + c0, nv, acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// nearest x2 upsample
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void upsample_fwd_kernel(int n, int h, int w, int c, const T* x, int x_ld, int x_off,
+                                    T* y, int y_ld, int y_off) {
+  const int G = (c + 7) >> 3;
+  const int H2 = 2 * h, W2 = 2 * w;
+  const long total = (long)n * H2 * W2 * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % G);
+    long r = t / G;
+    const int X = (int)(r % W2);
+    r /= W2;
+    const int Y = (int)(r % H2);
+    const int b = (int)(r / H2);
+    const int c0 = g * 8, nv = min(8, c - c0);
+    float v[8];
+    load8(x + (((long)b * h + (Y >> 1)) * w + (X >> 1)) * x_ld + x_off + c0, nv, v);
+    store8(y + (((long)b * H2 + Y) * W2 + X) * y_ld + y_off + c0, nv, v);
+  }
+}
+
+template <typename T>
+__global__ void upsample_bwd_kernel(int n, int h, int w, int c, const T* gy, int gy_ld, int gy_off,
+                                    T* gx, int gx_ld, int gx_off, int accumulate) {
+  const int G = (c + 7) >> 3;
+  const int W2 = 2 * w;
+  const long total = (long)n * h * w * G;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int g = (int)(t % G);
+    long r = t / G;
+    const int x = (int)(r % w);
+    r /= w;
+    const int y = (int)(r % h);
+    const int b = (int)(r / h);
+    const int c0 = g * 8, nv = min(8, c - c0);
+    float s[8];
+    T* dst = gx + (((long)b * h + y) * w + x) * gx_ld + gx_off + c0;
+    if (accumulate) load8(dst, nv, s);
+    else {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] = 0.f;
+    }
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      float v[8];
+      const int Y = 2 * y + (d >> 1), X = 2 * x + (d & 1);
+      load8(gy + (((long)b * 2 * h + Y) * W2 + X) * gy_ld + gy_off + c0, nv, v);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) s[i] += v[i];
+    }
+    store8(dst, nv, s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// layout / cast
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void pack_input_kernel(int n, int c, int h, int w, const float* x, T* y, int ld) {
+  const long npix = (long)n * h * w;
+  const long hw = (long)h * w;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < npix; t += (long)gridDim.x * blockDim.x) {
+    const long b = t / hw, s = t - b * hw;
+    for (int c0 = 0; c0 < ld; c0 += 8) {
+      float v[8];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = (c0 + i < c) ? x[(b * c + c0 + i) * hw + s] : 0.0f;
+      Vec8<T>::store(y + t * ld + c0, v);
+    }
+  }
+}
+
+// NHWC view -> NCHW contiguous, 64x64 (pixel x channel) tiles through LDS.
+template <typename TI, typename TO>
+__global__ void nhwc_to_nchw_kernel(int n, long hw, int c, const TI* x, int ld, int off, TO* y) {
+  __shared__ float tile[64][65];
+  const long pt = (long)blockIdx.x * 64;
+  const int ct = blockIdx.y * 64;
+  const int b = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const long p = pt + r;
+    const int ch = ct + tx;
+    tile[r][tx] = (p < hw && ch < c) ? (float)x[((long)b * hw + p) * ld + off + ch] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const int ch = ct + r;
+    const long p = pt + tx;
+    if (p < hw && ch < c) y[((long)b * c + ch) * hw + p] = (TO)tile[tx][r];
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void nchw_to_nhwc_kernel(int n, long hw, int c, const TI* x, TO* y, int ld, int off,
+                                    int accumulate) {
+  __shared__ float tile[64][65];
+  const long pt = (long)blockIdx.x * 64;
+  const int ct = blockIdx.y * 64;
+  const int b = blockIdx.z;
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  for (int r = ty; r < 64; r += 4) {
+    const int ch = ct + r;
+    const long p = pt + tx;
+    tile[r][tx] = (p < hw && ch < c) ? (float)x[((long)b * c + ch) * hw + p] : 0.f;
+  }
+  __syncthreads();
+  for (int r = ty; r < 64; r += 4) {
+    const long p = pt + r;
+    const int ch = ct + tx;
+    if (p < hw && ch < c) {
+      TO* d = y + ((long)b * hw + p) * ld + off + ch;
+      float v = tile[tx][r];
+      if (accumulate) v += (float)*d;
+      *d = (TO)v;
+    }
+  }
+}
+
+template <typename TI, typename TO>
+__global__ void cast_kernel(long count, const TI* x, TO* y) {
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < count; t += (long)gridDim.x * blockDim.x)
+    y[t] = (TO)(float)x[t];
+}
+
+}  // namespace yms
+
+using namespace yms;
+
+#define YMS_DT_DISPATCH(dt, T, ...)                 \
+  do {                                              \
+    if ((dt) == YMS_BF16) { typedef bf16 T; __VA_ARGS__; } \
+    else if ((dt) == YMS_F16) { typedef f16 T; __VA_ARGS__; } \
+    else if ((dt) == YMS_F32) { typedef float T; __VA_ARGS__; } \
+    else return YMS_ERR_INVALID;                    \
+  } while (0)
+
+static bool vok(int ld, int off, int c) { return c > 0 && ld % 8 == 0 && off % 8 == 0 && off + c <= ld; }
+
+extern "C" {
+
+yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float* rmean,
+                       const float* rvar, float eps, float* scale, float* shift, void* stream) {
+  if (c <= 0 || !scale || !shift) return YMS_ERR_INVALID;
+  if (gamma && (!beta || !rmean || !rvar)) return YMS_ERR_INVALID;
+  hipLaunchKernelGGL(bn_fold_kernel, dim3(cdiv(c, 256)), dim3(256), 0, (hipStream_t)stream, c, gamma,
+                     beta, rmean, rvar, eps, scale, shift);
+  return launch_status();
+}
+
+yms_status yms_bn_finalize(int c, const float* stats, int rows, int stats_ld, long count,
+                           const float* gamma, const float* beta, float* rmean, float* rvar,
+                           float momentum, float eps, float* mean_invstd, float* scale,
+                           float* shift, void* stream) {
+  if (c <= 0 || !stats || rows <= 0 || count <= 0 || !gamma || !beta || !mean_invstd || !scale || !shift)
+    return YMS_ERR_INVALID;
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, stats,
+                     rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps, mean_invstd, scale,
+                     shift);
+  return launch_status();
+}
+
+yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                          const float* scale, const float* shift, int act,
+                          const void* res, int res_ld, int res_off,
+                          void* y, int y_ld, int y_off, void* stream) {
+  if (npix <= 0 || !z || !y || !vok(z_ld, z_off, c) || !vok(y_ld, y_off, c)) return YMS_ERR_INVALID;
+  if (res && !vok(res_ld, res_off, c)) return YMS_ERR_INVALID;
+  const long items = npix * ((c + 7) / 8);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(affine_act_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
+                                               scale, shift, act, (const T*)res, res_ld, res_off, (T*)y,
+                                               y_ld, y_off));
+  return launch_status();
+}
+
+int yms_bn_bwd_rows(long npix) {
+  if (npix <= 0) return 0;
+  long rows = (npix + 255) / 256;
+  if (rows > 2048) rows = 2048;
+  return (int)rows;
+}
+
+static long bwd_pix_per_block(long npix) {
+  const int rows = yms_bn_bwd_rows(npix);
+  return (npix + rows - 1) / rows;
+}
+
+yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                                 const void* gy, int gy_ld, int gy_off, const float* scale,
+                                 const float* shift, const float* mean_invstd, int act,
+                                 float* ws, void* stream) {
+  if (npix <= 0 || !gy || !ws || !vok(gy_ld, gy_off, c)) return YMS_ERR_INVALID;
+  if (z && (!vok(z_ld, z_off, c) || !scale || !shift || !mean_invstd)) return YMS_ERR_INVALID;
+  const long ppb = bwd_pix_per_block(npix);
+  const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
+  if (z) {
+    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(rows), dim3(256), 0,
+                                                 (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
+                                                 (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd,
+                                                 act, ws, ppb));
+  } else {
+    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(rows), dim3(256), 0,
+                                                 (hipStream_t)stream, npix, c, (const T*)nullptr, 0, 0,
+                                                 (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd,
+                                                 act, ws, ppb));
+  }
+  return launch_status();
+}
+
+yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count, float* dgamma,
+                                   float* dbeta, float* coef, void* stream) {
+  if (c <= 0 || !ws || rows <= 0 || count <= 0) return YMS_ERR_INVALID;
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, ws,
+                     rows, count, dgamma, dbeta, coef);
+  return launch_status();
+}
+
+yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                                const void* gy, int gy_ld, int gy_off, const float* scale,
+                                const float* shift, const float* mean_invstd, const float* coef,
+                                int act, void* dz, int dz_ld, int dz_off,
+                                void* gres, int gres_ld, int gres_off, void* stream) {
+  if (npix <= 0 || !z || !gy || !dz || !scale || !shift || !mean_invstd || !coef) return YMS_ERR_INVALID;
+  if (!vok(z_ld, z_off, c) || !vok(gy_ld, gy_off, c) || !vok(dz_ld, dz_off, c)) return YMS_ERR_INVALID;
+  if (gres && !vok(gres_ld, gres_off, c)) return YMS_ERR_INVALID;
+  const long items = npix * ((c + 7) / 8);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
+                                               (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd, coef,
+                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off));
+  return launch_status();
+}
+
+yms_status yms_bias_bwd(int dtype, long npix, int c, const void* gy, int gy_ld, int gy_off,
+                        float* ws, float* dbias, void* stream) {
+  yms_status s = yms_bn_act_bwd_reduce(dtype, npix, c, nullptr, 0, 0, gy, gy_ld, gy_off, nullptr,
+                                       nullptr, nullptr, YMS_ACT_NONE, ws, stream);
+  if (s != YMS_OK) return s;
+  return yms_bn_act_bwd_finalize(c, ws, yms_bn_bwd_rows(npix), npix, nullptr, dbias, nullptr, stream);
+}
+
+size_t yms_sppf_ws_bytes(int n, int h, int w, int c) {
+  return (size_t)n * h * w * ((c + 7) / 8) * 8;
+}
+
+yms_status yms_sppf_pool_fwd(int dtype, int n, int h, int w, int c, void* buf, int ld, int off,
+                             void* stream) {
+  if (n <= 0 || h <= 0 || w <= 0 || !buf || !vok(ld, off, 4 * c) || c % 8 != 0) return YMS_ERR_INVALID;
+  const long items = (long)n * h * w * ((c + 7) / 8);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(sppf_fwd_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+                                               (hipStream_t)stream, n, h, w, c, (T*)buf, ld, off));
+  return launch_status();
+}
+
+yms_status yms_sppf_pool_bwd(int dtype, int n, int h, int w, int c, const void* buf, int ld,
+                             int off, void* gbuf, int gld, int goff, void* ws, void* stream) {
+  if (n <= 0 || !buf || !gbuf || !ws || !vok(ld, off, 4 * c) || !vok(gld, goff, 4 * c) || c % 8 != 0)
+    return YMS_ERR_INVALID;
+  if (ld != gld) return YMS_ERR_UNSUPPORTED;
+  const long items = (long)n * h * w * ((c + 7) / 8);
+  hipStream_t st = (hipStream_t)stream;
+  for (int k = 3; k >= 1; --k) {
+    // pool k reads slot k-1 (value buf) and produced slot k; push grad of slot k into slot k-1
+    YMS_DT_DISPATCH(dtype, T, {
+      hipLaunchKernelGGL(pool5_argmax_kernel<T>, dim3(grid_for(items)), dim3(256), 0, st, n, h, w, c,
+                         (const T*)buf, ld, off + (k - 1) * c, (uint8_t*)ws);
+      hipLaunchKernelGGL(pool5_gather_kernel<T>, dim3(grid_for(items)), dim3(256), 0, st, n, h, w, c,
+                         (const uint8_t*)ws, (T*)gbuf, gld, goff + (k - 1) * c, goff + k * c);
+    });
+  }
+  return launch_status();
+}
+
+yms_status yms_upsample2x_fwd(int dtype, int n, int h, int w, int c, const void* x, int x_ld,
+                              int x_off, void* y, int y_ld, int y_off, void* stream) {
+  if (n <= 0 || !x || !y || !vok(x_ld, x_off, c) || !vok(y_ld, y_off, c)) return YMS_ERR_INVALID;
+  const long items = (long)n * 4 * h * w * ((c + 7) / 8);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(upsample_fwd_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+                                               (hipStream_t)stream, n, h, w, c, (const T*)x, x_ld, x_off,
+                                               (T*)y, y_ld, y_off));
+  return launch_status();
+}
+
+yms_status yms_upsample2x_bwd(int dtype, int n, int h, int w, int c, const void* gy, int gy_ld,
+                              int gy_off, void* gx, int gx_ld, int gx_off, int accumulate,
+                              void* stream) {
+  if (n <= 0 || !gy || !gx || !vok(gy_ld, gy_off, c) || !vok(gx_ld, gx_off, c)) return YMS_ERR_INVALID;
+  const long items = (long)n * h * w * ((c + 7) / 8);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(upsample_bwd_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+                                               (hipStream_t)stream, n, h, w, c, (const T*)gy, gy_ld, gy_off,
+                                               (T*)gx, gx_ld, gx_off, accumulate));
+  return launch_status();
+}
+
+yms_status yms_pack_input(int dtype, int n, int c, int h, int w, const float* x, void* y, int ld,
+                          void* stream) {
+  if (n <= 0 || c <= 0 || !x || !y || ld % 8 != 0 || ld < c) return YMS_ERR_INVALID;
+  const long npix = (long)n * h * w;
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(pack_input_kernel<T>, dim3(grid_for(npix)), dim3(256), 0,
+                                               (hipStream_t)stream, n, c, h, w, x, (T*)y, ld));
+  return launch_status();
+}
+
+#define YMS_DT2(d1, d2, T1, T2, ...)                                          \
+  YMS_DT_DISPATCH(d1, T1, { YMS_DT_DISPATCH(d2, T2, __VA_ARGS__); })
+
+yms_status yms_nhwc_to_nchw(int dtype, int dtype_nchw, int n, int h, int w, int c, const void* x,
+                            int ld, int off, void* y, void* stream) {
+  if (n <= 0 || !x || !y || ld < off + c) return YMS_ERR_INVALID;
+  const long hw = (long)h * w;
+  dim3 grid((unsigned)cdiv(hw, 64), (unsigned)cdiv(c, 64), (unsigned)n);
+  YMS_DT2(dtype, dtype_nchw, TI, TO, hipLaunchKernelGGL((nhwc_to_nchw_kernel<TI, TO>), grid, dim3(256), 0,
+                                                        (hipStream_t)stream, n, hw, c, (const TI*)x, ld, off,
+                                                        (TO*)y));
+  return launch_status();
+}
+
+yms_status yms_nchw_to_nhwc(int dtype_nchw, int dtype, int n, int h, int w, int c, const void* x,
+                            void* y, int ld, int off, int accumulate, void* stream) {
+  if (n <= 0 || !x || !y || ld < off + c) return YMS_ERR_INVALID;
+  const long hw = (long)h * w;
+  dim3 grid((unsigned)cdiv(hw, 64), (unsigned)cdiv(c, 64), (unsigned)n);
+  YMS_DT2(dtype_nchw, dtype, TI, TO, hipLaunchKernelGGL((nchw_to_nhwc_kernel<TI, TO>), grid, dim3(256), 0,
+                                                        (hipStream_t)stream, n, hw, c, (const TI*)x, (TO*)y,
+                                                        ld, off, accumulate));
+  return launch_status();
+}
+
+yms_status yms_cast(int dtype_in, int dtype_out, long count, const void* x, void* y, void* stream) {
+  if (count <= 0 || !x || !y) return YMS_ERR_INVALID;
+  YMS_DT2(dtype_in, dtype_out, TI, TO, hipLaunchKernelGGL((cast_kernel<TI, TO>), dim3(grid_for(count)),
+                                                          dim3(256), 0, (hipStream_t)stream, count,
+                                                          (const TI*)x, (TO*)y));
+  return launch_status();
+}
+
+}  // extern "C"
+
+extern "C" yms_status yms_zero(void* p, size_t bytes, void* stream) {
+  if (!p) return YMS_ERR_INVALID;
+  if (bytes == 0) return YMS_OK;
+  return hipMemsetAsync(p, 0, bytes, (hipStream_t)stream) == hipSuccess ? YMS_OK : YMS_ERR_LAUNCH;
+}

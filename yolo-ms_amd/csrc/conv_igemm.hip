@@ -1,0 +1,787 @@
+// Implicit-GEMM convolution for gfx950 (MI355X) on MFMA, NHWC activations.
+//
+// Replaces the reference's Conv = Conv2d(bias=False) -> BatchNorm2d -> SiLU
+// (yolov8/model/components.py:69-77), its residual add (Bottleneck, :87-93), the channel
+// concatenations feeding C2f/SPPF/neck/head (:119, :146; yolov8_neck.py:79-91;
+// yolov8_head.py:122 -- producers write at a channel offset of the consumer's buffer),
+// the head's biased 1x1 nn.Conv2d (yolov8_head.py:86-109) and the autograd of all of them.
+//
+// GEMM views (rows = pixels, 16-B "chunks" of 8 bf16/f16 or 4 f32 channels along K):
+//   forward : Y[pix][co]  = sum_{tap,ci} X[src(pix,tap)][ci] * W[co][tap,ci]      (NT)
+//   dgrad   : DX[pix][ci] = sum_{tap,co} DZ[src'(pix,tap)][co] * W[co][ci][tap]    (NT)
+//   wgrad   : DW[co][tap,ci] = sum_pix DZ[pix][co] * X[src(pix,tap)][ci]           (TT)
+// NT tiles are staged global->regs->LDS as [rows][64 B of K] (80-B padded pitch, bank-
+// conflict-free for ds_read_b128) and consumed by v_mfma_f32_32x32x16_{bf16,f16}
+// (or v_mfma_f32_32x32x2_f32 for the exact-fp32 path).  TT tiles are staged as
+// [32 pixels][cols] and read with ds_read_b64_tr_b16 (hardware transpose) so both
+// operands get 8 consecutive pixels per lane.  wgrad is split over pixels into fp32
+// partial slabs that a second kernel reduces deterministically (no atomics).
+#include "yms_common.hpp"
+
+namespace yms {
+
+constexpr int NT_ROWP = 80;  // bytes per LDS row (64 B of K + 16 B pad)
+
+enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+enum { EPI_AFFINE = 0, EPI_STATS = 1, EPI_STORE = 2, EPI_ACCUM = 3 };
+
+struct NTParams {
+  const char* src;
+  const char* wp;
+  char* dst;
+  int src_ld, src_off, dst_ld, dst_off;
+  const float* scale;
+  const float* shift;
+  int act;
+  const char* res;
+  int res_ld, res_off;
+  float* stats;
+  int stats_ld;
+  int SH, SW;       // source spatial dims
+  int OW;           // row-space width
+  int stride, pad;
+  int cpt;          // 16-B chunks per tap along source channels
+  int Kc;           // valid K chunks
+  int nkt;          // K tiles (4 chunks each)
+  int M;            // rows (pixels)
+  int Ncols;        // valid output columns
+  int tiles_n;
+  FastDiv div_ow, div_ohw;
+};
+
+template <typename T> struct Mfma;
+template <> struct Mfma<bf16> {
+  static __device__ __forceinline__ f32x16 mma(const uint4& a, const uint4& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
+                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
+  }
+};
+template <> struct Mfma<f16> {
+  static __device__ __forceinline__ f32x16 mma(const uint4& a, const uint4& b, f32x16 c) {
+    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
+                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+  }
+};
+
+template <typename T>
+__device__ __forceinline__ void store_val(char* base, long idx, float v) {
+  reinterpret_cast<T*>(base)[idx] = (T)v;
+}
+
+template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN>
+__global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_SLOTS = BM / 64;
+  constexpr int B_CHUNKS = BN * 4;
+  constexpr int B_SLOTS = (B_CHUNKS + 255) / 256;
+  constexpr int TILE_BYTES = (BM + BN) * NT_ROWP;
+  constexpr bool F32 = sizeof(T) == 4;
+  static_assert(TM >= 1 && TN >= 1, "bad tile");
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tile_n = blockIdx.x % p.tiles_n, tile_m = blockIdx.x / p.tiles_n;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+
+  // ---- im2col loader state (A side): fixed chunk column q, rows r0 + 64*i ----
+  const int q = tid & 3, r0 = tid >> 2;
+  int a_base[A_SLOTS], a_y[A_SLOTS], a_x[A_SLOTS];
+  bool a_ok[A_SLOTS];
+#pragma unroll
+  for (int i = 0; i < A_SLOTS; ++i) {
+    const int m = m0 + r0 + 64 * i;
+    a_ok[i] = m < p.M;
+    const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
+    const uint32_t n = fdiv(mm, p.div_ohw);
+    const uint32_t rem = mm - n * p.div_ohw.d;
+    const uint32_t oy = fdiv(rem, p.div_ow);
+    const uint32_t ox = rem - oy * p.div_ow.d;
+    a_base[i] = (int)n * p.SH;
+    if (MODE == MODE_FWD) {
+      a_y[i] = (int)oy * p.stride - p.pad;
+      a_x[i] = (int)ox * p.stride - p.pad;
+    } else {
+      a_y[i] = (int)oy + p.pad;
+      a_x[i] = (int)ox + p.pad;
+    }
+  }
+  int tap = q / p.cpt, cc = q - (q / p.cpt) * p.cpt;
+
+  uint4 a_reg[A_SLOTS], b_reg[B_SLOTS];
+
+  auto load_tile = [&](int kt) {
+    const int kc = kt * 4 + q;
+    const int kh = tap / KS, kw = tap - (tap / KS) * KS;
+    const bool kok = kc < p.Kc;
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i) {
+      int iy, ix;
+      bool ok = kok && a_ok[i];
+      if (MODE == MODE_FWD) {
+        iy = a_y[i] + kh;
+        ix = a_x[i] + kw;
+      } else {
+        const int ty = a_y[i] - kh, tx = a_x[i] - kw;
+        if (p.stride == 2) {
+          ok = ok && ((ty | tx) & 1) == 0;
+          iy = ty >> 1;
+          ix = tx >> 1;
+        } else {
+          iy = ty;
+          ix = tx;
+        }
+      }
+      ok = ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW;
+      if (ok) {
+        const long e = ((long)(a_base[i] + iy) * p.SW + ix) * p.src_ld + p.src_off;
+        a_reg[i] = *reinterpret_cast<const uint4*>(p.src + e * sizeof(T) + cc * 16);
+      } else {
+        a_reg[i] = make_uint4(0, 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j) {
+      const int c = tid + 256 * j;
+      if (c < B_CHUNKS) {
+        const int row = c >> 2, qq = c & 3;
+        const long off = ((long)(n0 + row) * (p.nkt * 4) + kt * 4 + qq) * 16;
+        b_reg[j] = *reinterpret_cast<const uint4*>(p.wp + off);
+      }
+    }
+    // advance the tap cursor by 4 chunks for the next k-tile
+    cc += 4;
+    while (cc >= p.cpt) { cc -= p.cpt; ++tap; }
+  };
+
+  auto store_tile = [&](int buf) {
+    char* A = smem + buf * TILE_BYTES;
+    char* B = A + BM * NT_ROWP;
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i)
+      *reinterpret_cast<uint4*>(A + (r0 + 64 * i) * NT_ROWP + q * 16) = a_reg[i];
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j) {
+      const int c = tid + 256 * j;
+      if (c < B_CHUNKS) *reinterpret_cast<uint4*>(B + (c >> 2) * NT_ROWP + (c & 3) * 16) = b_reg[j];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.0f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  auto compute = [&](int buf) {
+    const char* A = smem + buf * TILE_BYTES;
+    const char* B = A + BM * NT_ROWP;
+    if constexpr (!F32) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint4 af[TM], bfr[TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          af[a] = *reinterpret_cast<const uint4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bfr[b] = *reinterpret_cast<const uint4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[a], bfr[b], acc[a][b]);
+      }
+    } else {
+      // fp32: lane (r,h) holds k = 8h..8h+7 of its row; MFMA j pairs element j of both halves.
+      float af[TM][8], bfr[TN][8];
+#pragma unroll
+      for (int a = 0; a < TM; ++a) {
+        const float4* src = reinterpret_cast<const float4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 32 * lh);
+        float4 u = src[0], v = src[1];
+        af[a][0] = u.x; af[a][1] = u.y; af[a][2] = u.z; af[a][3] = u.w;
+        af[a][4] = v.x; af[a][5] = v.y; af[a][6] = v.z; af[a][7] = v.w;
+      }
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const float4* src = reinterpret_cast<const float4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 32 * lh);
+        float4 u = src[0], v = src[1];
+        bfr[b][0] = u.x; bfr[b][1] = u.y; bfr[b][2] = u.z; bfr[b][3] = u.w;
+        bfr[b][4] = v.x; bfr[b][5] = v.y; bfr[b][6] = v.z; bfr[b][7] = v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][j], bfr[b][j], acc[a][b], 0, 0, 0);
+    }
+  };
+
+  // ---- main loop: register-staged double buffer, one barrier per k-tile ----
+  load_tile(0);
+  store_tile(0);
+  __syncthreads();
+  for (int kt = 0; kt < p.nkt; ++kt) {
+    const int cur = kt & 1;
+    const bool more = kt + 1 < p.nkt;
+    if (more) load_tile(kt + 1);
+    compute(cur);
+    if (more) store_tile(cur ^ 1);
+    __syncthreads();
+  }
+
+  // ---- epilogue ----
+  float s1[TN], s2[TN];
+#pragma unroll
+  for (int b = 0; b < TN; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+#pragma unroll
+  for (int b = 0; b < TN; ++b) {
+    const int col = n0 + wn * WTN + b * 32 + lr;
+    const bool col_ok = col < p.Ncols;
+    float sc = 1.0f, sh = 0.0f;
+    if (EPI == EPI_AFFINE && col_ok) {
+      if (p.scale) sc = p.scale[col];
+      if (p.shift) sh = p.shift[col];
+    }
+#pragma unroll
+    for (int a = 0; a < TM; ++a) {
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        float v = acc[a][b][i];
+        if (EPI == EPI_STATS) {
+          s1[b] += v;
+          s2[b] += v * v;
+        }
+        if (row < p.M && col_ok) {
+          if (EPI == EPI_AFFINE) {
+            v = v * sc + sh;
+            if (p.act == YMS_ACT_SILU) v = silu_f(v);
+            if (p.res) v += (float)reinterpret_cast<const T*>(p.res)[(long)row * p.res_ld + p.res_off + col];
+          } else if (EPI == EPI_ACCUM) {
+            v += (float)reinterpret_cast<const T*>(p.dst)[(long)row * p.dst_ld + p.dst_off + col];
+          }
+          store_val<T>(p.dst, (long)row * p.dst_ld + p.dst_off + col, v);
+        }
+      }
+    }
+  }
+  if (EPI == EPI_STATS) {
+    float* red = reinterpret_cast<float*>(smem);  // [WGM][2][BN]
+#pragma unroll
+    for (int b = 0; b < TN; ++b) {
+      float t1 = s1[b] + __shfl_xor(s1[b], 32);
+      float t2 = s2[b] + __shfl_xor(s2[b], 32);
+      if (lh == 0) {
+        red[(wm * 2 + 0) * BN + wn * WTN + b * 32 + lr] = t1;
+        red[(wm * 2 + 1) * BN + wn * WTN + b * 32 + lr] = t2;
+      }
+    }
+    __syncthreads();
+    if (tid < BN) {
+      float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+      for (int w = 0; w < WGM; ++w) {
+        t1 += red[(w * 2 + 0) * BN + tid];
+        t2 += red[(w * 2 + 1) * BN + tid];
+      }
+      float* st = p.stats + (long)tile_m * 2 * p.stats_ld;
+      st[n0 + tid] = t1;
+      st[p.stats_ld + n0 + tid] = t2;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// wgrad: TT GEMM over pixels with ds_read_b64_tr_b16 operands, split-K partial slabs.
+// ------------------------------------------------------------------------------------------
+struct TTParams {
+  const char* x;
+  const char* dz;
+  float* slab;
+  int x_ld, x_off, dz_ld, dz_off;
+  int SH, SW, OW, stride, pad;
+  int cpt;       // chunks per tap of x channels
+  int Kc;        // valid kf chunks
+  int M;         // pixels (rows of dz)
+  int cout8;     // cout rounded up to 8 (valid dz channels incl. zero pad)
+  int nkt;       // pixel tiles of 32
+  int kt_per_split;
+  int tiles_n;   // kf tiles
+  int slab_rows, slab_ld;
+  FastDiv div_ow, div_ohw;
+};
+
+template <typename T, int KS, int BM, int BN>
+__global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
+  constexpr int WGM = 2, WGN = 2;
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int SZ = sizeof(T);
+  constexpr bool F32 = SZ == 4;
+  constexpr int EPC = 16 / SZ;                 // elements per chunk
+  constexpr int PA = BM * SZ + 64, PB = BN * SZ + 64;   // LDS pitches (conflict-free tr reads)
+  constexpr int CA = BM / EPC, CB = BN / EPC;  // chunks per LDS row
+  constexpr int A_SLOTS = (32 * CA + 255) / 256, B_SLOTS = (32 * CB + 255) / 256;
+  constexpr int TILE = 32 * (PA + PB);
+  __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int tile_n = blockIdx.x % p.tiles_n, tile_m = blockIdx.x / p.tiles_n;
+  const int split = blockIdx.y;
+  const int m0 = tile_m * BM, n0 = tile_n * BN;
+  const int kt0 = split * p.kt_per_split;
+  const int kt1 = min(p.nkt, kt0 + p.kt_per_split);
+
+  // B-side (x im2col) chunk columns are fixed per slot: precompute tap decomposition.
+  int b_row[B_SLOTS], b_kh[B_SLOTS], b_kw[B_SLOTS], b_cc[B_SLOTS], b_col[B_SLOTS];
+  bool b_kok[B_SLOTS];
+#pragma unroll
+  for (int j = 0; j < B_SLOTS; ++j) {
+    const int c = tid + 256 * j;
+    b_row[j] = c / CB;
+    b_col[j] = c - b_row[j] * CB;
+    const int kc = n0 / EPC + b_col[j];
+    b_kok[j] = (c < 32 * CB) && kc < p.Kc;
+    const int t = kc / p.cpt;
+    b_cc[j] = kc - t * p.cpt;
+    b_kh[j] = t / KS;
+    b_kw[j] = t - b_kh[j] * KS;
+  }
+  uint4 a_reg[A_SLOTS], b_reg[B_SLOTS];
+
+  auto load_tile = [&](int kt) {
+    const int q0 = kt * 32;
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i) {
+      const int c = tid + 256 * i;
+      const int row = c / CA, col = c - (c / CA) * CA;
+      const int qpix = q0 + row;
+      const int ch = m0 + col * EPC;
+      if (c < 32 * CA && qpix < p.M && ch < p.cout8)
+        a_reg[i] = *reinterpret_cast<const uint4*>(p.dz + ((long)qpix * p.dz_ld + p.dz_off + ch) * SZ);
+      else
+        a_reg[i] = make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j) {
+      const int qpix = q0 + b_row[j];
+      bool ok = b_kok[j] && qpix < p.M;
+      const uint32_t mm = ok ? (uint32_t)qpix : 0u;
+      const uint32_t n = fdiv(mm, p.div_ohw);
+      const uint32_t rem = mm - n * p.div_ohw.d;
+      const uint32_t oy = fdiv(rem, p.div_ow);
+      const uint32_t ox = rem - oy * p.div_ow.d;
+      const int iy = (int)oy * p.stride - p.pad + b_kh[j];
+      const int ix = (int)ox * p.stride - p.pad + b_kw[j];
+      ok = ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW;
+      if (ok) {
+        const long e = (((long)n * p.SH + iy) * p.SW + ix) * p.x_ld + p.x_off;
+        b_reg[j] = *reinterpret_cast<const uint4*>(p.x + e * SZ + b_cc[j] * 16);
+      } else {
+        b_reg[j] = make_uint4(0, 0, 0, 0);
+      }
+    }
+  };
+  auto store_tile = [&](int buf) {
+    char* A = smem + buf * TILE;
+    char* B = A + 32 * PA;
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i) {
+      const int c = tid + 256 * i;
+      if (c < 32 * CA) *reinterpret_cast<uint4*>(A + (c / CA) * PA + (c % CA) * 16) = a_reg[i];
+    }
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j) {
+      const int c = tid + 256 * j;
+      if (c < 32 * CB) *reinterpret_cast<uint4*>(B + b_row[j] * PB + b_col[j] * 16) = b_reg[j];
+    }
+  };
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.0f;
+
+  const int lr = lane & 31, lh = lane >> 5;
+  // tr-read lane geometry (16-lane groups): group g, block row qq, column quad pp
+  const int g = lane >> 4, gi = lane & 15, qq = gi >> 2, pp = gi & 3;
+  const int th = g >> 1, tcb = 16 * (g & 1);
+
+  auto compute = [&](int buf) {
+    const char* A = smem + buf * TILE;
+    const char* B = A + 32 * PA;
+    if constexpr (!F32) {
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        uint4 af[TM], bfr[TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a) {
+          const int col = wm * WTM + a * 32 + tcb + 4 * pp;
+          const int row = 16 * s + 8 * th + qq;
+          const YMS_LDS s16x4* p0 = (const YMS_LDS s16x4*)(A + row * PA + col * 2);
+          const YMS_LDS s16x4* p1 = (const YMS_LDS s16x4*)(A + (row + 4) * PA + col * 2);
+          s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p0);
+          s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p1);
+          uint2 u0 = __builtin_bit_cast(uint2, v0), u1 = __builtin_bit_cast(uint2, v1);
+          af[a] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+        }
+#pragma unroll
+        for (int b = 0; b < TN; ++b) {
+          const int col = wn * WTN + b * 32 + tcb + 4 * pp;
+          const int row = 16 * s + 8 * th + qq;
+          const YMS_LDS s16x4* p0 = (const YMS_LDS s16x4*)(B + row * PB + col * 2);
+          const YMS_LDS s16x4* p1 = (const YMS_LDS s16x4*)(B + (row + 4) * PB + col * 2);
+          s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p0);
+          s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p1);
+          uint2 u0 = __builtin_bit_cast(uint2, v0), u1 = __builtin_bit_cast(uint2, v1);
+          bfr[b] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+        }
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[a], bfr[b], acc[a][b]);
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        float av[TM], bv[TN];
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          av[a] = *reinterpret_cast<const float*>(A + (2 * j + lh) * PA + (wm * WTM + a * 32 + lr) * 4);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bv[b] = *reinterpret_cast<const float*>(B + (2 * j + lh) * PB + (wn * WTN + b * 32 + lr) * 4);
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int b = 0; b < TN; ++b)
+            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[a], bv[b], acc[a][b], 0, 0, 0);
+      }
+    }
+  };
+
+  if (kt0 < kt1) {
+    load_tile(kt0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = kt0; kt < kt1; ++kt) {
+      const int cur = (kt - kt0) & 1;
+      const bool more = kt + 1 < kt1;
+      if (more) load_tile(kt + 1);
+      compute(cur);
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+    }
+  }
+  float* slab = p.slab + (long)split * p.slab_rows * p.slab_ld;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        const int col = n0 + wn * WTN + b * 32 + lr;
+        slab[(long)row * p.slab_ld + col] = acc[a][b][i];
+      }
+}
+
+// dw[co][ci][kh][kw] (+)= sum_s slab[s][co][tap*cin8 + ci]; threads walk the slab order.
+__global__ void wgrad_reduce_kernel(const float* slab, int splits, long slab_elems, int slab_ld,
+                                    int cout, int cin, int cin8, int ks, float* dw, int accumulate) {
+  const long total = (long)cout * ks * ks * cin8;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int ci = (int)(t % cin8);
+    const long r = t / cin8;
+    const int tap = (int)(r % (ks * ks));
+    const int co = (int)(r / (ks * ks));
+    if (ci >= cin) continue;
+    const long sidx = (long)co * slab_ld + (long)tap * cin8 + ci;
+    float s = 0.f;
+    for (int z = 0; z < splits; ++z) s += slab[z * slab_elems + sidx];
+    const long o = (((long)co * cin + ci) * ks + tap / ks) * ks + tap % ks;
+    dw[o] = accumulate ? dw[o] + s : s;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// weight packing
+// ------------------------------------------------------------------------------------------
+template <typename T>
+__global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, int ks, int rows,
+                                   int kp_elems, int c8_in, int for_dgrad) {
+  // fwd  : out[co][tap*cin8 + ci]   = w[co][ci][tap]        rows = cout_pad
+  // dgrad: out[ci][tap*cout8 + co]  = w[co][ci][tap]        rows = cin_pad
+  const long total = (long)rows * kp_elems;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int r = (int)(t / kp_elems);
+    const int k = (int)(t % kp_elems);
+    const int tap = k / c8_in, c = k % c8_in;
+    float v = 0.f;
+    if (tap < ks * ks) {
+      const int co = for_dgrad ? c : r;
+      const int ci = for_dgrad ? r : c;
+      if (co < cout && ci < cin) v = w[((long)co * cin + ci) * ks * ks + tap];
+    }
+    out[t] = (T)v;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// host side
+// ------------------------------------------------------------------------------------------
+static int elem_size(int dt) { return dt == YMS_F32 ? 4 : 2; }
+
+struct PackGeo {
+  int rows, c8_in, cpt, kc, nkt, kp_elems;
+};
+static PackGeo pack_geo(const yms_conv_shape* s, int for_dgrad) {
+  PackGeo g;
+  const int es = elem_size(s->dtype);
+  const int cin_k = for_dgrad ? s->cout : s->cin;    // channels along K
+  const int cout_r = for_dgrad ? s->cin : s->cout;   // rows
+  g.c8_in = (int)rup(cin_k, 8);
+  g.cpt = g.c8_in * es / 16;
+  g.kc = s->k * s->k * g.cpt;
+  g.nkt = cdiv(g.kc, 4);
+  g.kp_elems = g.nkt * 64 / es;
+  g.rows = (int)rup(cout_r, 128);
+  return g;
+}
+
+static bool shape_ok(const yms_conv_shape* s) {
+  if (!s || s->n <= 0 || s->h <= 0 || s->w <= 0 || s->cin <= 0 || s->cout <= 0) return false;
+  if (!(s->k == 1 || s->k == 3) || !(s->stride == 1 || s->stride == 2)) return false;
+  if (s->dtype < 0 || s->dtype > 2) return false;
+  if (s->ho != (s->h + 2 * s->pad - s->k) / s->stride + 1) return false;
+  if (s->wo != (s->w + 2 * s->pad - s->k) / s->stride + 1) return false;
+  if ((long)s->n * s->h * s->w >= (1l << 31) || (long)s->n * s->ho * s->wo >= (1l << 31)) return false;
+  return true;
+}
+static bool view_ok(int ld, int off, int c) { return ld % 8 == 0 && off % 8 == 0 && off + c <= ld; }
+
+struct TileChoice { int cfg, bn; };
+static TileChoice choose_tile(int ncols) {
+  // minimise padded columns; prefer wider tiles on ties
+  const int bns[3] = {128, 64, 32};
+  int best = 0;
+  long bestpad = 1l << 40;
+  for (int i = 0; i < 3; ++i) {
+    long pad = rup(ncols, bns[i]);
+    if (pad < bestpad) { bestpad = pad; best = i; }
+  }
+  return TileChoice{best, bns[best]};
+}
+
+template <typename T, int KS, int MODE, int EPI>
+static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
+  NTParams p = p0;
+  if (cfg == 0) {
+    p.tiles_n = cdiv(p.Ncols, 128);
+    dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n));
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 128, 2, 2>), grid, dim3(256), 0, st, p);
+  } else if (cfg == 1) {
+    p.tiles_n = cdiv(p.Ncols, 64);
+    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n));
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 256, 64, 4, 1>), grid, dim3(256), 0, st, p);
+  } else {
+    p.tiles_n = cdiv(p.Ncols, 32);
+    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n));
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 256, 32, 4, 1>), grid, dim3(256), 0, st, p);
+  }
+}
+
+template <int MODE, int EPI>
+static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hipStream_t st) {
+#define YMS_NT_CASE(T)                                          \
+  if (ks == 1) launch_nt<T, 1, MODE, EPI>(p, cfg, st);          \
+  else launch_nt<T, 3, MODE, EPI>(p, cfg, st);
+  if (dtype == YMS_BF16) { YMS_NT_CASE(bf16) }
+  else if (dtype == YMS_F16) { YMS_NT_CASE(f16) }
+  else { YMS_NT_CASE(float) }
+#undef YMS_NT_CASE
+  return launch_status();
+}
+
+static int rows_for(int M, int cfg) { return cdiv(M, cfg == 0 ? 128 : 256); }
+
+struct WgradPlan {
+  int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc;
+};
+static WgradPlan wgrad_plan(const yms_conv_shape* s) {
+  WgradPlan w;
+  const int es = elem_size(s->dtype);
+  w.cin8 = (int)rup(s->cin, 8);
+  w.cpt = w.cin8 * es / 16;
+  w.kc = s->k * s->k * w.cpt;
+  const int kf = s->k * s->k * w.cin8;
+  w.bm = s->cout <= 64 ? 64 : 128;
+  w.bn = kf <= 64 ? 64 : 128;
+  w.tiles_m = cdiv(s->cout, w.bm);
+  w.tiles_n = cdiv(kf, w.bn);
+  w.slab_rows = w.tiles_m * w.bm;
+  w.slab_ld = w.tiles_n * w.bn;
+  const long M = (long)s->n * s->ho * s->wo;
+  w.nkt = cdiv(M, 32);
+  const int blocks = w.tiles_m * w.tiles_n;
+  int splits = std::max(1, std::min(w.nkt, cdiv(2048, blocks)));
+  w.kt_per_split = cdiv(w.nkt, splits);
+  w.splits = cdiv(w.nkt, w.kt_per_split);
+  return w;
+}
+
+template <typename T, int KS>
+static void launch_wgrad(const TTParams& p, int bm, int bn, dim3 grid, hipStream_t st) {
+  if (bm == 64 && bn == 64) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 64>), grid, dim3(256), 0, st, p);
+  else if (bm == 64) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 128>), grid, dim3(256), 0, st, p);
+  else if (bn == 64) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 64>), grid, dim3(256), 0, st, p);
+  else hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 128>), grid, dim3(256), 0, st, p);
+}
+
+}  // namespace yms
+
+using namespace yms;
+
+extern "C" {
+
+size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad) {
+  if (!shape_ok(s)) return 0;
+  PackGeo g = pack_geo(s, for_dgrad);
+  return (size_t)g.rows * g.kp_elems;
+}
+
+yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* packed,
+                                int for_dgrad, void* stream) {
+  if (!shape_ok(s) || !w || !packed) return YMS_ERR_INVALID;
+  PackGeo g = pack_geo(s, for_dgrad);
+  hipStream_t st = (hipStream_t)stream;
+  const long total = (long)g.rows * g.kp_elems;
+  dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 4096));
+  if (s->dtype == YMS_BF16)
+    hipLaunchKernelGGL(pack_weight_kernel<bf16>, grid, dim3(256), 0, st, w, (bf16*)packed, s->cout, s->cin, s->k, g.rows, g.kp_elems, g.c8_in, for_dgrad);
+  else if (s->dtype == YMS_F16)
+    hipLaunchKernelGGL(pack_weight_kernel<f16>, grid, dim3(256), 0, st, w, (f16*)packed, s->cout, s->cin, s->k, g.rows, g.kp_elems, g.c8_in, for_dgrad);
+  else
+    hipLaunchKernelGGL(pack_weight_kernel<float>, grid, dim3(256), 0, st, w, (float*)packed, s->cout, s->cin, s->k, g.rows, g.kp_elems, g.c8_in, for_dgrad);
+  return launch_status();
+}
+
+int yms_conv_stats_rows(const yms_conv_shape* s) {
+  if (!shape_ok(s)) return 0;
+  TileChoice tc = choose_tile(s->cout);
+  return rows_for(s->n * s->ho * s->wo, tc.cfg);
+}
+int yms_conv_stats_ld(const yms_conv_shape* s) {
+  if (!shape_ok(s)) return 0;
+  return (int)rup(s->cout, 128);
+}
+
+yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
+                        const void* wpacked, void* y, int y_ld, int y_off,
+                        const float* scale, const float* shift, int act,
+                        const void* res, int res_ld, int res_off, float* stats, void* stream) {
+  if (!shape_ok(s) || !x || !wpacked || !y) return YMS_ERR_INVALID;
+  if (!view_ok(x_ld, x_off, s->cin) || !view_ok(y_ld, y_off, s->cout)) return YMS_ERR_INVALID;
+  if (res && !view_ok(res_ld, res_off, s->cout)) return YMS_ERR_INVALID;
+  const int es = elem_size(s->dtype);
+  PackGeo g = pack_geo(s, 0);
+  NTParams p{};
+  p.src = (const char*)x;
+  p.wp = (const char*)wpacked;
+  p.dst = (char*)y;
+  p.src_ld = x_ld; p.src_off = x_off; p.dst_ld = y_ld; p.dst_off = y_off;
+  p.scale = scale; p.shift = shift; p.act = act;
+  p.res = (const char*)res; p.res_ld = res_ld; p.res_off = res_off;
+  p.stats = stats;
+  p.stats_ld = (int)rup(s->cout, 128);
+  p.SH = s->h; p.SW = s->w; p.OW = s->wo;
+  p.stride = s->stride; p.pad = s->pad;
+  p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
+  p.M = s->n * s->ho * s->wo;
+  p.Ncols = s->cout;
+  p.div_ow = make_fastdiv(s->wo);
+  p.div_ohw = make_fastdiv(s->ho * s->wo);
+  (void)es;
+  TileChoice tc = choose_tile(s->cout);
+  hipStream_t st = (hipStream_t)stream;
+  if (stats) return dispatch_nt<MODE_FWD, EPI_STATS>(p, s->dtype, s->k, tc.cfg, st);
+  return dispatch_nt<MODE_FWD, EPI_AFFINE>(p, s->dtype, s->k, tc.cfg, st);
+}
+
+yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
+                          const void* wpacked_t, void* dx, int dx_ld, int dx_off,
+                          int accumulate, void* stream) {
+  if (!shape_ok(s) || !dz || !wpacked_t || !dx) return YMS_ERR_INVALID;
+  if (!view_ok(dz_ld, dz_off, s->cout) || !view_ok(dx_ld, dx_off, s->cin)) return YMS_ERR_INVALID;
+  PackGeo g = pack_geo(s, 1);
+  NTParams p{};
+  p.src = (const char*)dz;
+  p.wp = (const char*)wpacked_t;
+  p.dst = (char*)dx;
+  p.src_ld = dz_ld; p.src_off = dz_off; p.dst_ld = dx_ld; p.dst_off = dx_off;
+  p.SH = s->ho; p.SW = s->wo; p.OW = s->w;
+  p.stride = s->stride; p.pad = s->pad;
+  p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
+  p.M = s->n * s->h * s->w;
+  p.Ncols = s->cin;
+  p.div_ow = make_fastdiv(s->w);
+  p.div_ohw = make_fastdiv(s->h * s->w);
+  TileChoice tc = choose_tile(s->cin);
+  hipStream_t st = (hipStream_t)stream;
+  if (accumulate) return dispatch_nt<MODE_DGRAD, EPI_ACCUM>(p, s->dtype, s->k, tc.cfg, st);
+  return dispatch_nt<MODE_DGRAD, EPI_STORE>(p, s->dtype, s->k, tc.cfg, st);
+}
+
+size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s) {
+  if (!shape_ok(s)) return 0;
+  WgradPlan w = wgrad_plan(s);
+  return (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float);
+}
+
+yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
+                          const void* dz, int dz_ld, int dz_off, float* ws, size_t ws_bytes,
+                          float* dw, int accumulate, void* stream) {
+  if (!shape_ok(s) || !x || !dz || !ws || !dw) return YMS_ERR_INVALID;
+  if (!view_ok(x_ld, x_off, s->cin) || !view_ok(dz_ld, dz_off, s->cout)) return YMS_ERR_INVALID;
+  WgradPlan w = wgrad_plan(s);
+  if (ws_bytes < (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
+  TTParams p{};
+  p.x = (const char*)x; p.dz = (const char*)dz; p.slab = ws;
+  p.x_ld = x_ld; p.x_off = x_off; p.dz_ld = dz_ld; p.dz_off = dz_off;
+  p.SH = s->h; p.SW = s->w; p.OW = s->wo; p.stride = s->stride; p.pad = s->pad;
+  p.cpt = w.cpt; p.Kc = w.kc;
+  p.M = s->n * s->ho * s->wo;
+  p.cout8 = (int)rup(s->cout, 8);
+  p.nkt = w.nkt; p.kt_per_split = w.kt_per_split; p.tiles_n = w.tiles_n;
+  p.slab_rows = w.slab_rows; p.slab_ld = w.slab_ld;
+  p.div_ow = make_fastdiv(s->wo);
+  p.div_ohw = make_fastdiv(s->ho * s->wo);
+  hipStream_t st = (hipStream_t)stream;
+  dim3 grid((unsigned)(w.tiles_m * w.tiles_n), (unsigned)w.splits);
+  if (s->dtype == YMS_BF16) {
+    if (s->k == 1) launch_wgrad<bf16, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<bf16, 3>(p, w.bm, w.bn, grid, st);
+  } else if (s->dtype == YMS_F16) {
+    if (s->k == 1) launch_wgrad<f16, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<f16, 3>(p, w.bm, w.bn, grid, st);
+  } else {
+    if (s->k == 1) launch_wgrad<float, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<float, 3>(p, w.bm, w.bn, grid, st);
+  }
+  yms_status e = launch_status();
+  if (e != YMS_OK) return e;
+  const long total = (long)s->cout * s->k * s->k * w.cin8;
+  dim3 g2((unsigned)std::min<long>(cdiv(total, 256), 8192));
+  hipLaunchKernelGGL(wgrad_reduce_kernel, g2, dim3(256), 0, st, ws, w.splits,
+                     (long)w.slab_rows * w.slab_ld, w.slab_ld, s->cout, s->cin, w.cin8, s->k, dw, accumulate);
+  return launch_status();
+}
+
+}  // extern "C"

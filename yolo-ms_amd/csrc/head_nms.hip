@@ -1,0 +1,427 @@
+// Detection-head decode and batched class-wise NMS for gfx950.
+//
+// decode  : yolov8/model/yolov8_head.py:127-158 (make_anchors, DFL softmax-expectation from
+//           components.py:162-191, ltrb -> cxcywh, x stride, sigmoid(cls)), fused with the
+//           post-process prep of tools/train.py:63-78 (xyxy, max/argmax over classes, score >
+//           conf).  Computed in fp32 whatever the activation dtype.
+// NMS     : replaces the per-image, per-class Python loop of train.py:80-101 around
+//           torchvision.ops.nms (train.py:93).  One workgroup per (image, class): ordered
+//           (stable) compaction of that class' candidates, bitonic sort on the key
+//           (descending score, ascending anchor id) == torch's stable descending sort,
+//           then the greedy suppression in 64-candidate blocks: a block is first tested
+//           against every box already kept (all 4 waves), then resolved sequentially inside
+//           one wave.  IoU arithmetic is torchvision's CPU kernel op-for-op (fp32, no +1,
+//           ratio compared as double), FP contraction disabled, so keep indices are
+//           bit-exact against the CPU oracle on identical decoded inputs.
+#include "yms_common.hpp"
+
+#pragma clang fp contract(off)
+
+namespace yms {
+
+struct DecodeParams {
+  const void* lvl[4];
+  int h[4], w[4];
+  int aoff[5];
+  float stride[4];
+  int nlev, no_ld, nc, A, n;
+  float conf;
+  float* out;
+  float* bxy;
+  float* score;
+  int* label;
+};
+
+template <typename T>
+__global__ void head_decode_kernel(DecodeParams p) {
+  const long total = (long)p.n * p.A;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int b = (int)(t / p.A);
+    const int a = (int)(t - (long)b * p.A);
+    int l = 0;
+    while (l + 1 < p.nlev && a >= p.aoff[l + 1]) ++l;
+    const int r = a - p.aoff[l];
+    const int y = r / p.w[l], x = r - (r / p.w[l]) * p.w[l];
+    const T* src = reinterpret_cast<const T*>(p.lvl[l]) + (((long)b * p.h[l] + y) * p.w[l] + x) * p.no_ld;
+    float d[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      float v[16];
+      float vv[8];
+      Vec8<T>::load(src + 16 * k, vv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] = vv[i];
+      Vec8<T>::load(src + 16 * k + 8, vv);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[8 + i] = vv[i];
+      float m = v[0];
+#pragma unroll
+      for (int i = 1; i < 16; ++i) m = fmaxf(m, v[i]);
+      float s = 0.f, e = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const float ex = expf(v[i] - m);
+        s += ex;
+        e += ex * (float)i;
+      }
+      d[k] = e / s;
+    }
+    const float ax = (float)x + 0.5f, ay = (float)y + 0.5f, st = p.stride[l];
+    const float a0 = ax - d[0], a1 = ay - d[1];
+    const float b0 = ax + d[2], b1 = ay + d[3];
+    const float cx = ((a0 + b0) / 2) * st, cy = ((a1 + b1) / 2) * st;
+    const float bw = (b0 - a0) * st, bh = (b1 - a1) * st;
+    float* o = p.out + t * (4 + p.nc);
+    o[0] = cx; o[1] = cy; o[2] = bw; o[3] = bh;
+    float best = 0.f;
+    int bl = 0;
+    const T* cls = src + 64;
+    for (int c = 0; c < p.nc; ++c) {
+      const float pr = 1.0f / (1.0f + expf(-(float)cls[c]));
+      o[4 + c] = pr;
+      if (c == 0 || pr > best) { best = pr; bl = c; }
+    }
+    if (p.score) {
+      p.bxy[t * 4 + 0] = cx - bw / 2;
+      p.bxy[t * 4 + 1] = cy - bh / 2;
+      p.bxy[t * 4 + 2] = cx + bw / 2;
+      p.bxy[t * 4 + 3] = cy + bh / 2;
+      p.score[t] = best;
+      p.label[t] = best > p.conf ? bl : -1;
+    }
+  }
+}
+
+__global__ void nms_prep_kernel(int n, int A, int nc, const float* pred, float conf, float* bxy,
+                                float* score, int* label) {
+  const long total = (long)n * A;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const float* q = pred + t * (4 + nc);
+    const float cx = q[0], cy = q[1], w = q[2], h = q[3];
+    bxy[t * 4 + 0] = cx - w / 2;
+    bxy[t * 4 + 1] = cy - h / 2;
+    bxy[t * 4 + 2] = cx + w / 2;
+    bxy[t * 4 + 3] = cy + h / 2;
+    float best = q[4];
+    int bl = 0;
+    for (int c = 1; c < nc; ++c)
+      if (q[4 + c] > best) { best = q[4 + c]; bl = c; }
+    score[t] = best;
+    label[t] = best > conf ? bl : -1;
+  }
+}
+
+// ---------------------------------------------------------------------------------------
+// class-wise NMS
+// ---------------------------------------------------------------------------------------
+constexpr int NMS_CAP = 1024;
+
+__device__ __forceinline__ uint32_t orderable(float f) {
+  uint32_t u = __float_as_uint(f);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__device__ __forceinline__ bool iou_gt(const float4& i, const float4& j, double thr) {
+  const float iarea = (i.z - i.x) * (i.w - i.y);
+  const float jarea = (j.z - j.x) * (j.w - j.y);
+  const float xx1 = fmaxf(i.x, j.x);
+  const float yy1 = fmaxf(i.y, j.y);
+  const float xx2 = fminf(i.z, j.z);
+  const float yy2 = fminf(i.w, j.w);
+  const float w = fmaxf(0.0f, xx2 - xx1);
+  const float h = fmaxf(0.0f, yy2 - yy1);
+  const float inter = w * h;
+  const float ovr = inter / (iarea + jarea - inter);
+  return (double)ovr > thr;
+}
+
+struct NmsWs {
+  uint64_t* gkeys;   // [n][A]
+  float4* gboxes;    // [n][A]
+  int* scratch;      // [n][A]
+  int* cls_cnt;      // [n][nc]
+  int* cls_off;      // [n][nc]
+};
+
+__global__ __launch_bounds__(256) void nms_class_kernel(int A, int nc, const float* bxy,
+                                                        const float* score, const int* label,
+                                                        double thr, NmsWs ws) {
+  __shared__ uint64_t s_keys[NMS_CAP];
+  __shared__ float4 s_boxes[NMS_CAP];
+  __shared__ int s_red[2][4];
+  __shared__ int s_nkept;
+  __shared__ unsigned long long s_sup[4];
+
+  const int c = blockIdx.x, b = blockIdx.y;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int* lab = label ? label + (long)b * A : nullptr;
+
+  // pass 1: count (label < c) and (label == c)
+  int lt = 0, eq = 0;
+  for (int a = tid; a < A; a += 256) {
+    const int l = lab ? lab[a] : 0;
+    lt += (l >= 0 && l < c);
+    eq += (l == c);
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    lt += __shfl_xor(lt, o);
+    eq += __shfl_xor(eq, o);
+  }
+  if (lane == 0) { s_red[0][wave] = lt; s_red[1][wave] = eq; }
+  __syncthreads();
+  const int off = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
+  const int n = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
+  if (tid == 0) {
+    ws.cls_off[(long)b * nc + c] = off;
+    ws.cls_cnt[(long)b * nc + c] = 0;
+  }
+  if (n == 0) return;
+  const bool big = n > NMS_CAP;
+  uint64_t* keys = big ? ws.gkeys + (long)b * A + off : s_keys;
+  float4* boxes = big ? ws.gboxes + (long)b * A + off : s_boxes;
+  int* out = ws.scratch + (long)b * A + off;
+  const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
+  const float* sc = score + (long)b * A;
+  __syncthreads();
+
+  // pass 2: stable ordered compaction of this class' anchors into keys
+  int base = 0;
+  for (int a0 = 0; a0 < A; a0 += 256) {
+    const int a = a0 + tid;
+    const bool f = a < A && (lab ? lab[a] == c : true);
+    const unsigned long long m = __ballot(f);
+    const int pre = __popcll(m & ((1ull << lane) - 1ull));
+    if (lane == 0) s_red[0][wave] = __popcll(m);
+    __syncthreads();
+    int wpre = 0, tot = 0;
+#pragma unroll
+    for (int w = 0; w < 4; ++w) {
+      const int cnt = s_red[0][w];
+      wpre += (w < wave) ? cnt : 0;
+      tot += cnt;
+    }
+    if (f) {
+      const uint32_t okey = ~orderable(sc[a]);
+      keys[base + wpre + pre] = ((uint64_t)okey << 32) | (uint32_t)a;
+    }
+    base += tot;
+    __syncthreads();
+  }
+
+  // bitonic sort (direction-free flip formulation; virtual +inf padding beyond n)
+  int N2 = 1;
+  while (N2 < n) N2 <<= 1;
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int t = tid; t < N2; t += 256) {
+        const int partner = (j == (k >> 1)) ? (t ^ (k - 1)) : (t ^ j);
+        if (partner > t && partner < n) {
+          const uint64_t x = keys[t], y = keys[partner];
+          if (y < x) { keys[t] = y; keys[partner] = x; }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  // gather boxes in sorted order
+  for (int i = tid; i < n; i += 256) boxes[i] = bx[(uint32_t)keys[i]];
+  if (tid == 0) s_nkept = 0;
+  __syncthreads();
+
+  for (int blk = 0; blk < n; blk += 64) {
+    const int m = min(64, n - blk);
+    const int j = tid & 63;
+    const bool has = j < m;
+    float4 cb = has ? boxes[blk + j] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const uint32_t cidx = has ? (uint32_t)keys[blk + j] : 0u;
+    const int nk = s_nkept;
+    bool sup = false;
+    if (has)
+      for (int k = wave; k < nk; k += 4) {
+        if (iou_gt(boxes[k], cb, thr)) { sup = true; break; }
+      }
+    const unsigned long long sm = __ballot(sup);
+    if (lane == 0) s_sup[wave] = sm;
+    __syncthreads();
+    if (wave == 0) {
+      const unsigned long long allsup = s_sup[0] | s_sup[1] | s_sup[2] | s_sup[3];
+      bool alive = has && !((allsup >> j) & 1ull);
+      for (int i = 0; i < m; ++i) {
+        const bool ai = (__ballot(alive) >> i) & 1ull;
+        if (!ai) continue;
+        float4 bi;
+        bi.x = __shfl(cb.x, i);
+        bi.y = __shfl(cb.y, i);
+        bi.z = __shfl(cb.z, i);
+        bi.w = __shfl(cb.w, i);
+        if (alive && j > i && iou_gt(bi, cb, thr)) alive = false;
+      }
+      const unsigned long long km = __ballot(alive);
+      const int pos = nk + __popcll(km & ((1ull << lane) - 1ull));
+      if (alive) {
+        boxes[pos] = cb;      // compact kept boxes to the front (pos <= blk + j)
+        out[pos] = (int)cidx;
+      }
+      if (lane == 0) s_nkept = nk + __popcll(km);
+    }
+    __syncthreads();
+  }
+  if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nkept;
+}
+
+__global__ void nms_compact_kernel(int A, int nc, NmsWs ws, int64_t* keep_idx, int* keep_lbl,
+                                   int* counts) {
+  const int b = blockIdx.x;
+  int pos = 0;
+  for (int c = 0; c < nc; ++c) {
+    const int cnt = ws.cls_cnt[(long)b * nc + c];
+    const int off = ws.cls_off[(long)b * nc + c];
+    for (int k = threadIdx.x; k < cnt; k += blockDim.x) {
+      keep_idx[(long)b * A + pos + k] = ws.scratch[(long)b * A + off + k];
+      if (keep_lbl) keep_lbl[(long)b * A + pos + k] = c;
+    }
+    pos += cnt;
+  }
+  if (threadIdx.x == 0) counts[b] = pos;
+}
+
+static size_t r256(size_t x) { return (x + 255) & ~(size_t)255; }
+static NmsWs carve(void* ws, int n, int A, int nc) {
+  char* p = (char*)ws;
+  NmsWs w;
+  w.gkeys = (uint64_t*)p;
+  p += r256((size_t)n * A * 8);
+  w.gboxes = (float4*)p;
+  p += r256((size_t)n * A * 16);
+  w.scratch = (int*)p;
+  p += r256((size_t)n * A * 4);
+  w.cls_cnt = (int*)p;
+  p += r256((size_t)n * nc * 4);
+  w.cls_off = (int*)p;
+  return w;
+}
+
+}  // namespace yms
+
+using namespace yms;
+
+extern "C" {
+
+const char* yms_version(void) { return "yms-mi355x 0.1 (gfx950)"; }
+
+const char* yms_status_string(yms_status s) {
+  switch (s) {
+    case YMS_OK: return "ok";
+    case YMS_ERR_INVALID: return "invalid argument";
+    case YMS_ERR_UNSUPPORTED: return "unsupported configuration";
+    case YMS_ERR_LAUNCH: return "kernel launch failed";
+    default: return "unknown status";
+  }
+}
+
+yms_status yms_head_decode(int dtype, int n, int nc, int nlev, const void* const* lvl,
+                           const int* hs, const int* ws, int no_ld, const float* strides,
+                           float* out, float conf, float* boxes_xyxy, float* nms_score,
+                           int* label, void* stream) {
+  if (n <= 0 || nc <= 0 || nlev <= 0 || nlev > 4 || !lvl || !hs || !ws || !strides || !out) return YMS_ERR_INVALID;
+  if (no_ld % 8 != 0 || no_ld < 64 + nc) return YMS_ERR_INVALID;
+  if (nms_score && (!boxes_xyxy || !label)) return YMS_ERR_INVALID;
+  DecodeParams p{};
+  int A = 0;
+  for (int l = 0; l < nlev; ++l) {
+    if (!lvl[l] || hs[l] <= 0 || ws[l] <= 0) return YMS_ERR_INVALID;
+    p.lvl[l] = lvl[l];
+    p.h[l] = hs[l];
+    p.w[l] = ws[l];
+    p.aoff[l] = A;
+    p.stride[l] = strides[l];
+    A += hs[l] * ws[l];
+  }
+  p.aoff[nlev] = A;
+  p.nlev = nlev; p.no_ld = no_ld; p.nc = nc; p.A = A; p.n = n; p.conf = conf;
+  p.out = out; p.bxy = boxes_xyxy; p.score = nms_score; p.label = label;
+  const long total = (long)n * A;
+  dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 16384));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == YMS_BF16) hipLaunchKernelGGL(head_decode_kernel<bf16>, grid, dim3(256), 0, st, p);
+  else if (dtype == YMS_F16) hipLaunchKernelGGL(head_decode_kernel<f16>, grid, dim3(256), 0, st, p);
+  else if (dtype == YMS_F32) hipLaunchKernelGGL(head_decode_kernel<float>, grid, dim3(256), 0, st, p);
+  else return YMS_ERR_INVALID;
+  return launch_status();
+}
+
+yms_status yms_nms_prep(int n, int A, int nc, const float* pred, float conf, float* boxes_xyxy,
+                        float* score, int* label, void* stream) {
+  if (n <= 0 || A <= 0 || nc <= 0 || !pred || !boxes_xyxy || !score || !label) return YMS_ERR_INVALID;
+  const long total = (long)n * A;
+  hipLaunchKernelGGL(nms_prep_kernel, dim3((unsigned)std::min<long>(cdiv(total, 256), 16384)), dim3(256), 0,
+                     (hipStream_t)stream, n, A, nc, pred, conf, boxes_xyxy, score, label);
+  return launch_status();
+}
+
+size_t yms_nms_ws_bytes(int n, int A, int nc) {
+  return r256((size_t)n * A * 8) + r256((size_t)n * A * 16) + r256((size_t)n * A * 4) +
+         r256((size_t)n * nc * 4) + r256((size_t)n * nc * 4);
+}
+
+yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, const float* score,
+                             const int* label, double iou, int64_t* keep_idx, int* keep_lbl,
+                             int* counts, void* ws, size_t ws_bytes, void* stream) {
+  if (n <= 0 || A <= 0 || nc <= 0 || !boxes_xyxy || !score || !keep_idx || !counts || !ws) return YMS_ERR_INVALID;
+  if (ws_bytes < yms_nms_ws_bytes(n, A, nc)) return YMS_ERR_INVALID;
+  if ((uintptr_t)ws % 16 != 0 || (uintptr_t)boxes_xyxy % 16 != 0) return YMS_ERR_INVALID;
+  NmsWs w = carve(ws, n, A, nc);
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(nms_class_kernel, dim3((unsigned)nc, (unsigned)n), dim3(256), 0, st, A, nc, boxes_xyxy,
+                     score, label, iou, w);
+  yms_status e = launch_status();
+  if (e != YMS_OK) return e;
+  hipLaunchKernelGGL(nms_compact_kernel, dim3((unsigned)n), dim3(256), 0, st, A, nc, w, keep_idx, keep_lbl,
+                     counts);
+  return launch_status();
+}
+
+yms_status yms_nms_single(int m, const float* boxes, const float* scores, double iou,
+                          int64_t* keep, int* count, void* ws, size_t ws_bytes, void* stream) {
+  if (m <= 0 || !boxes || !scores || !keep || !count) return YMS_ERR_INVALID;
+  return yms_nms_classwise(1, m, 1, boxes, scores, nullptr, iou, keep, nullptr, count, ws, ws_bytes, stream);
+}
+
+}  // extern "C"
+
+// ---------------------------------------------------------------------------------------
+// standalone DFL integral (components.py:186-191): x [n][4*ch][A] -> out [n][4][A]
+// ---------------------------------------------------------------------------------------
+namespace yms {
+template <typename T>
+__global__ void dfl_kernel(int n, int A, int ch, const T* x, T* out) {
+  const long total = (long)n * 4 * A;
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    const int a = (int)(t % A);
+    const long bk = t / A;            // b*4 + k
+    const T* src = x + bk * ch * (long)A + a;
+    float m = -INFINITY;
+    for (int j = 0; j < ch; ++j) m = fmaxf(m, (float)src[(long)j * A]);
+    float s = 0.f, e = 0.f;
+    for (int j = 0; j < ch; ++j) {
+      const float ex = expf((float)src[(long)j * A] - m);
+      s += ex;
+      e += ex * (float)j;
+    }
+    out[t] = (T)(e / s);
+  }
+}
+}  // namespace yms
+
+extern "C" yms_status yms_dfl(int dtype, int n, int A, int ch, const void* x, void* out, void* stream) {
+  if (n <= 0 || A <= 0 || ch <= 0 || !x || !out) return YMS_ERR_INVALID;
+  const long total = (long)n * 4 * A;
+  dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 16384));
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == YMS_BF16) hipLaunchKernelGGL(dfl_kernel<bf16>, grid, dim3(256), 0, st, n, A, ch, (const bf16*)x, (bf16*)out);
+  else if (dtype == YMS_F16) hipLaunchKernelGGL(dfl_kernel<f16>, grid, dim3(256), 0, st, n, A, ch, (const f16*)x, (f16*)out);
+  else if (dtype == YMS_F32) hipLaunchKernelGGL(dfl_kernel<float>, grid, dim3(256), 0, st, n, A, ch, (const float*)x, (float*)out);
+  else return YMS_ERR_INVALID;
+  return launch_status();
+}

@@ -1,0 +1,118 @@
+"""ctypes binding of libyms.so (C-ABI declared in include/yms.h).
+
+The HIP library is mandatory: there is no CPU or eager-PyTorch fallback.  If the
+shared object is missing or a call returns a non-zero status, a RuntimeError is
+raised immediately.  torch must be imported before the library is loaded so that
+libyms.so binds to the HIP runtime already loaded by torch (same soname).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import torch  # noqa: F401  (loads the process' HIP runtime first)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libyms.so")
+
+F32, BF16, F16 = 0, 1, 2
+ACT_NONE, ACT_SILU = 0, 1
+
+_DT = {torch.float32: F32, torch.bfloat16: BF16, torch.float16: F16}
+
+
+def dtype_code(dt):
+    try:
+        return _DT[dt]
+    except KeyError:
+        raise RuntimeError(f"yms: unsupported dtype {dt}; use float32, bfloat16 or float16") from None
+
+
+class ConvShape(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int) for k in
+                ("n", "h", "w", "cin", "cout", "k", "stride", "pad", "ho", "wo", "dtype")]
+
+
+_P = ctypes.c_void_p
+_I = ctypes.c_int
+_L = ctypes.c_long
+_F = ctypes.c_float
+_D = ctypes.c_double
+_SZ = ctypes.c_size_t
+_SP = ctypes.POINTER(ConvShape)
+
+_SIGS = {
+    "yms_version": (ctypes.c_char_p, []),
+    "yms_status_string": (ctypes.c_char_p, [_I]),
+    "yms_conv_packed_elems": (_SZ, [_SP, _I]),
+    "yms_conv_pack_weight": (_I, [_SP, _P, _P, _I, _P]),
+    "yms_conv_stats_rows": (_I, [_SP]),
+    "yms_conv_stats_ld": (_I, [_SP]),
+    "yms_conv_fwd": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _P]),
+    "yms_conv_dgrad": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
+    "yms_conv_wgrad_ws_bytes": (_SZ, [_SP]),
+    "yms_conv_wgrad": (_I, [_SP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
+    "yms_bn_fold": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
+    "yms_bn_finalize": (_I, [_I, _P, _I, _I, _L, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P]),
+    "yms_affine_act": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _I, _I, _P]),
+    "yms_bn_bwd_rows": (_I, [_L]),
+    "yms_bn_act_bwd_reduce": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
+    "yms_bn_act_bwd_finalize": (_I, [_I, _P, _I, _L, _P, _P, _P, _P]),
+    "yms_bn_act_bwd_apply": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _I, _P, _I, _I,
+                                  _P, _I, _I, _P]),
+    "yms_bias_bwd": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _P]),
+    "yms_sppf_ws_bytes": (_SZ, [_I, _I, _I, _I]),
+    "yms_sppf_pool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P]),
+    "yms_sppf_pool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P]),
+    "yms_upsample2x_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P]),
+    "yms_upsample2x_bwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P]),
+    "yms_pack_input": (_I, [_I, _I, _I, _I, _I, _P, _P, _I, _P]),
+    "yms_nhwc_to_nchw": (_I, [_I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _P]),
+    "yms_nchw_to_nhwc": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
+    "yms_cast": (_I, [_I, _I, _L, _P, _P, _P]),
+    "yms_zero": (_I, [_P, _SZ, _P]),
+    "yms_head_decode": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P]),
+    "yms_dfl": (_I, [_I, _I, _I, _I, _P, _P, _P]),
+    "yms_nms_prep": (_I, [_I, _I, _I, _P, _F, _P, _P, _P, _P]),
+    "yms_nms_ws_bytes": (_SZ, [_I, _I, _I]),
+    "yms_nms_classwise": (_I, [_I, _I, _I, _P, _P, _P, _D, _P, _P, _P, _P, _SZ, _P]),
+    "yms_nms_single": (_I, [_I, _P, _P, _D, _P, _P, _P, _SZ, _P]),
+}
+
+EXPORTED = tuple(_SIGS)
+_lib = None
+
+
+def lib():
+    """Load libyms.so (raises RuntimeError when the HIP extension has not been built)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(
+                f"yms: HIP library {LIB_PATH} not found -- build it with "
+                "`python -c 'import __graft_entry__ as g; g.build()'` (make -C yolo-ms_amd/csrc)")
+        L = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(L, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = L
+    return _lib
+
+
+def check(status, what):
+    if status != 0:
+        msg = lib().yms_status_string(status).decode()
+        raise RuntimeError(f"yms: {what} failed: {msg} (status {status})")
+
+
+def call(name, *args):
+    check(getattr(lib(), name)(*args), name)
+
+
+def stream_ptr(device=None):
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def ptr(t):
+    return None if t is None else t.data_ptr()

@@ -1,0 +1,453 @@
+"""Static execution plans for the YOLOv8 / YOLO-MS detector graph on MI355X.
+
+A plan is built once per (module, input shape, compute dtype, train/eval) by walking
+the module tree (each yolov8 module implements ``emit``).  It records
+
+* NHWC activation buffers (channel stride ``ld`` = round8(C)) laid out in one arena;
+  every channel concatenation of the reference (C2f ``torch.cat`` at
+  components.py:119, SPPF :146, neck yolov8_neck.py:79-91, head yolov8_head.py:122)
+  is a *placement*: producers write at a channel offset of the consumer's buffer,
+  so no copy kernel exists;
+* a list of ops (ConvOp, BiasConvOp, UpsampleOp, SppfPoolOp, InputOp) whose
+  forward/backward are launches of the hand-written HIP kernels in libyms.so.
+
+Training: forward stores the pre-BN conv output z, BN batch statistics are fused in
+the conv epilogue (per-tile partial sums) and finalised by one tiny kernel which also
+updates running_mean/var exactly like nn.BatchNorm2d(eps=1e-3, momentum=0.03).
+Backward walks the ops in reverse: BN+SiLU backward (two-pass reduction), dgrad and
+wgrad implicit GEMMs, fp32 parameter gradients written into one flat arena (ordered
+in backward-completion order so that data-parallel all-reduce buckets complete
+contiguously -- see yms.dist).
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from . import _lib as L
+
+ALIGN = 256
+BN_MOMENTUM = 0.03   # components.py:73
+BN_EPS = 1e-3
+
+
+def r8(c):
+    return (c + 7) // 8 * 8
+
+
+def _al(x):
+    return (x + ALIGN - 1) // ALIGN * ALIGN
+
+
+class Buf:
+    __slots__ = ("idx", "n", "h", "w", "ld", "name", "off", "zero", "needs_grad")
+
+    def __init__(self, idx, n, h, w, ld, name, zero):
+        self.idx, self.n, self.h, self.w, self.ld, self.name, self.zero = idx, n, h, w, ld, name, zero
+        self.off = None
+        self.needs_grad = True
+
+    @property
+    def npix(self):
+        return self.n * self.h * self.w
+
+
+class View:
+    __slots__ = ("buf", "off", "c")
+
+    def __init__(self, buf, off, c):
+        self.buf, self.off, self.c = buf, off, c
+
+    def slot(self, k, c):
+        """Channel sub-view [off + k, off + k + c) (8-aligned: the kernels move 16-B chunks)."""
+        if (self.off + k) % 8:
+            raise RuntimeError(f"yms: channel slice at offset {self.off + k} is not a multiple of 8")
+        return View(self.buf, self.off + k, c)
+
+    @property
+    def h(self):
+        return self.buf.h
+
+    @property
+    def w(self):
+        return self.buf.w
+
+
+class Layout:
+    """Arena allocator used while finalising a plan (byte offsets)."""
+
+    def __init__(self):
+        self.size = 0
+
+    def alloc(self, nbytes):
+        off = self.size
+        self.size += _al(max(int(nbytes), 1))
+        return off
+
+
+class Rt:
+    """Per-call runtime state."""
+
+    def __init__(self, plan, base, stream, training):
+        self.plan = plan
+        self.base = base
+        self.gbase = None
+        self.st = stream
+        self.training = training
+        self.pg_base = None      # flat fp32 param-grad arena pointer
+        self.eval_base = None    # eval cache base pointer (packed weights + folded BN)
+
+    def a(self, v):
+        return self.base + v.buf.off
+
+    def g(self, v):
+        return self.gbase + v.buf.off
+
+
+class ConvOp:
+    """Conv block = Conv2d(bias=False) -> BatchNorm2d -> SiLU/Identity (+ residual),
+    components.py:69-77 (residual: Bottleneck :87-93)."""
+
+    def __init__(self, b, mod, x, y, res, act):
+        conv = mod.conv
+        if conv.groups != 1 or conv.dilation != (1, 1) or conv.kernel_size[0] != conv.kernel_size[1]:
+            raise RuntimeError("yms: only square, ungrouped, undilated convolutions are supported")
+        if conv.stride[0] != conv.stride[1] or conv.padding[0] != conv.padding[1]:
+            raise RuntimeError("yms: anisotropic stride/padding unsupported")
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        self.mod, self.x, self.y, self.res, self.act = mod, x, y, res, act
+        self.shape = L.ConvShape(b.n, x.h, x.w, conv.in_channels, conv.out_channels, k, s, p,
+                                 y.h, y.w, b.dt)
+        self.sp = ctypes.pointer(self.shape)
+        self.c = conv.out_channels
+        self.npix = b.n * y.h * y.w
+        self.pw = b.param(conv, "weight")
+        self.pg = b.param(mod.bn, "weight")
+        self.pb = b.param(mod.bn, "bias")
+        self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
+
+    def layout(self, plan, La, Le):
+        es = plan.es
+        self.wp_elems = L.lib().yms_conv_packed_elems(self.sp, 0)
+        self.wpt_elems = L.lib().yms_conv_packed_elems(self.sp, 1)
+        c = self.c
+        # eval cache: packed fwd weights + folded scale/shift
+        self.e_wp = Le.alloc(self.wp_elems * es)
+        self.e_sc = Le.alloc(4 * c)
+        self.e_sh = Le.alloc(4 * c)
+        if plan.training:
+            self.zld = r8(c)
+            self.z = La.alloc(self.npix * self.zld * es)
+            self.t_wp = La.alloc(self.wp_elems * es)
+            self.t_wpt = La.alloc(self.wpt_elems * es)
+            self.sc = La.alloc(4 * c)
+            self.sh = La.alloc(4 * c)
+            self.mi = La.alloc(8 * c)
+            self.stats_rows = L.lib().yms_conv_stats_rows(self.sp)
+            self.stats_ld = L.lib().yms_conv_stats_ld(self.sp)
+            plan.need_scratch("stats", 4 * 2 * self.stats_rows * self.stats_ld)
+            plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix))
+            plan.need_scratch("coef", 8 * c)
+            plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
+
+    def prepare_eval(self, rt):
+        m = self.mod
+        L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), rt.eval_base + self.e_wp, 0, rt.st)
+        bn = m.bn
+        L.call("yms_bn_fold", self.c, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+               bn.running_var.data_ptr(), ctypes.c_float(bn.eps), rt.eval_base + self.e_sc,
+               rt.eval_base + self.e_sh, rt.st)
+
+    def fwd(self, rt):
+        x, y, r = self.x, self.y, self.res
+        xl, yl = x.buf.ld, y.buf.ld
+        rp = rt.a(r) if r is not None else None
+        rl, ro = (r.buf.ld, r.off) if r is not None else (0, 0)
+        if not rt.training:
+            eb = rt.eval_base
+            L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, eb + self.e_wp, rt.a(y), yl, y.off,
+                   eb + self.e_sc, eb + self.e_sh, self.act, rp, rl, ro, None, rt.st)
+            return
+        m = self.mod
+        base = rt.base
+        L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wp, 0, rt.st)
+        L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wpt, 1, rt.st)
+        stats = base + rt.plan.scratch["stats"]
+        L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
+               None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
+        bn = m.bn
+        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
+               bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+               ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
+               ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
+        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+               base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
+
+    def bwd(self, rt):
+        x, y, r = self.x, self.y, self.res
+        base, dt, c = rt.base, rt.plan.dt, self.c
+        gy, gyl, gyo = rt.g(y), y.buf.ld, y.off
+        ws = rt.gbase + rt.plan.gscratch["bwd"]
+        coef = rt.gbase + rt.plan.gscratch["coef"]
+        z = base + self.z
+        L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+               base + self.sh, base + self.mi, self.act, ws, rt.st)
+        L.call("yms_bn_act_bwd_finalize", c, ws, L.lib().yms_bn_bwd_rows(self.npix), self.npix,
+               rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        gres = rt.g(r) if r is not None else None
+        gro = (r.buf.ld, r.off) if r is not None else (0, 0)
+        L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+               base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, gres, gro[0], gro[1], rt.st)
+        if x.buf.needs_grad:
+            L.call("yms_conv_dgrad", self.sp, z, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off, 1, rt.st)
+        dw = rt.pgrad(self.pw)
+        if dw is not None:
+            wsz = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
+            L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
+                   rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.st)
+
+    def grad_params(self):
+        return [self.pb, self.pg, self.pw]
+
+
+class BiasConvOp:
+    """Plain nn.Conv2d with bias (the head's final 1x1 layers, yolov8_head.py:86-109)."""
+
+    def __init__(self, b, conv, x, y):
+        if conv.groups != 1 or conv.bias is None:
+            raise RuntimeError("yms: biased ungrouped conv expected")
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        self.conv, self.x, self.y = conv, x, y
+        self.shape = L.ConvShape(b.n, x.h, x.w, conv.in_channels, conv.out_channels, k, s, p, y.h, y.w, b.dt)
+        self.sp = ctypes.pointer(self.shape)
+        self.c = conv.out_channels
+        self.npix = b.n * y.h * y.w
+        self.pw = b.param(conv, "weight")
+        self.pbias = b.param(conv, "bias")
+        self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
+
+    def layout(self, plan, La, Le):
+        es = plan.es
+        self.wp_elems = L.lib().yms_conv_packed_elems(self.sp, 0)
+        self.wpt_elems = L.lib().yms_conv_packed_elems(self.sp, 1)
+        self.e_wp = Le.alloc(self.wp_elems * es)
+        if plan.training:
+            self.t_wp = La.alloc(self.wp_elems * es)
+            self.t_wpt = La.alloc(self.wpt_elems * es)
+            plan.need_scratch("bwd", 4 * 2 * self.c * L.lib().yms_bn_bwd_rows(self.npix))
+            plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
+
+    def prepare_eval(self, rt):
+        L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), rt.eval_base + self.e_wp, 0, rt.st)
+
+    def fwd(self, rt):
+        x, y = self.x, self.y
+        if rt.training:
+            wp = rt.base + self.t_wp
+            L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), wp, 0, rt.st)
+            L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), rt.base + self.t_wpt, 1, rt.st)
+        else:
+            wp = rt.eval_base + self.e_wp
+        L.call("yms_conv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, wp, rt.a(y), y.buf.ld, y.off,
+               None, self.conv.bias.data_ptr(), L.ACT_NONE, None, 0, 0, None, rt.st)
+
+    def bwd(self, rt):
+        x, y = self.x, self.y
+        gy, gyl, gyo = rt.g(y), y.buf.ld, y.off
+        db = rt.pgrad(self.pbias)
+        if db is not None:
+            L.call("yms_bias_bwd", rt.plan.dt, self.npix, self.c, gy, gyl, gyo,
+                   rt.gbase + rt.plan.gscratch["bwd"], db, rt.st)
+        if x.buf.needs_grad:
+            L.call("yms_conv_dgrad", self.sp, gy, gyl, gyo, rt.base + self.t_wpt, rt.g(x), x.buf.ld, x.off, 1, rt.st)
+        dw = rt.pgrad(self.pw)
+        if dw is not None:
+            L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, gy, gyl, gyo,
+                   rt.gbase + rt.plan.gscratch["wgrad"], L.lib().yms_conv_wgrad_ws_bytes(self.sp), dw, 0, rt.st)
+
+    def grad_params(self):
+        return [self.pbias, self.pw]
+
+
+class UpsampleOp:
+    """nearest x2, components.py:153-160."""
+
+    def __init__(self, b, x, y):
+        self.x, self.y, self.n = x, y, b.n
+        self.flops = 0
+
+    def layout(self, plan, La, Le):
+        pass
+
+    def fwd(self, rt):
+        x, y = self.x, self.y
+        L.call("yms_upsample2x_fwd", rt.plan.dt, self.n, x.h, x.w, x.c, rt.a(x), x.buf.ld, x.off,
+               rt.a(y), y.buf.ld, y.off, rt.st)
+
+    def bwd(self, rt):
+        x, y = self.x, self.y
+        L.call("yms_upsample2x_bwd", rt.plan.dt, self.n, x.h, x.w, x.c, rt.g(y), y.buf.ld, y.off,
+               rt.g(x), x.buf.ld, x.off, 1, rt.st)
+
+    def grad_params(self):
+        return []
+
+
+class SppfPoolOp:
+    """The three chained MaxPool2d(5,1,2) of SPPF (components.py:136-146) over a 4-slot buffer."""
+
+    def __init__(self, b, v4, c):
+        self.v, self.c, self.n = v4, c, b.n
+        self.flops = 0
+
+    def layout(self, plan, La, Le):
+        if plan.training:
+            plan.need_scratch("sppf", L.lib().yms_sppf_ws_bytes(self.n, self.v.h, self.v.w, self.c))
+
+    def fwd(self, rt):
+        v = self.v
+        L.call("yms_sppf_pool_fwd", rt.plan.dt, self.n, v.h, v.w, self.c, rt.a(v), v.buf.ld, v.off, rt.st)
+
+    def bwd(self, rt):
+        v = self.v
+        L.call("yms_sppf_pool_bwd", rt.plan.dt, self.n, v.h, v.w, self.c, rt.a(v), v.buf.ld, v.off,
+               rt.g(v), v.buf.ld, v.off, rt.gbase + rt.plan.gscratch["sppf"], rt.st)
+
+    def grad_params(self):
+        return []
+
+
+class Builder:
+    """Collects buffers, ops and parameter references while modules ``emit``."""
+
+    def __init__(self, n, dt, training):
+        self.n, self.dt, self.training = n, dt, training
+        self.es = 4 if dt == L.F32 else 2
+        self.bufs = []
+        self.ops = []
+        self.param_refs = []      # (module, attr)
+        self._pidx = {}
+
+    def new(self, h, w, c, name="act", ld=None):
+        b = Buf(len(self.bufs), self.n, h, w, ld if ld is not None else r8(c), name, zero=(c % 8 != 0))
+        self.bufs.append(b)
+        return View(b, 0, c)
+
+    def param(self, mod, attr):
+        key = (id(mod), attr)
+        if key not in self._pidx:
+            self._pidx[key] = len(self.param_refs)
+            self.param_refs.append((mod, attr))
+        return self._pidx[key]
+
+    # --- emitters used by the yolov8 modules -------------------------------------------
+    def conv(self, mod, x, out=None, res=None, act=None):
+        conv = mod.conv
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        ho, wo = (x.h + 2 * p - k) // s + 1, (x.w + 2 * p - k) // s + 1
+        if out is None:
+            out = self.new(ho, wo, conv.out_channels)
+        assert out.c == conv.out_channels and out.h == ho and out.w == wo, "yms: output view mismatch"
+        if act is None:
+            act = L.ACT_SILU if isinstance(mod.activation, torch.nn.SiLU) else L.ACT_NONE
+        self.ops.append(ConvOp(self, mod, x, out, res, act))
+        return out
+
+    def conv2d_bias(self, conv, x, out=None):
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        ho, wo = (x.h + 2 * p - k) // s + 1, (x.w + 2 * p - k) // s + 1
+        if out is None:
+            out = self.new(ho, wo, conv.out_channels)
+        self.ops.append(BiasConvOp(self, conv, x, out))
+        return out
+
+    def upsample(self, x, out=None):
+        if out is None:
+            out = self.new(2 * x.h, 2 * x.w, x.c)
+        self.ops.append(UpsampleOp(self, x, out))
+        return out
+
+    def sppf_pool(self, v4, c):
+        self.ops.append(SppfPoolOp(self, v4, c))
+
+
+class Plan:
+    def __init__(self, b: Builder, inputs, outputs, kind):
+        self.n, self.dt, self.training, self.es = b.n, b.dt, b.training, b.es
+        self.bufs, self.ops, self.param_refs = b.bufs, b.ops, b.param_refs
+        self.inputs, self.outputs, self.kind = inputs, outputs, kind
+        self.scratch_req = {}
+        La, Le = Layout(), Layout()
+        for buf in self.bufs:
+            buf.off = La.alloc(buf.npix * buf.ld * self.es)
+        self.act_bytes = La.size
+        for op in self.ops:
+            op.layout(self, La, Le)
+        self.scratch = {}
+        if self.training:
+            self.scratch["stats"] = La.alloc(self.scratch_req.get("stats", 0))
+        self.arena_bytes = La.size
+        # grad arena: activation grads share the activation layout, then backward scratch
+        Lg = Layout()
+        Lg.size = self.act_bytes
+        self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf")}
+        self.garena_bytes = Lg.size
+        self.eval_bytes = Le.size
+        self.zero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.zero]
+        self.flops = sum(op.flops for op in self.ops)
+        # parameter-gradient arena in backward-completion order (reverse op order)
+        order = []
+        seen = set()
+        for op in reversed(self.ops):
+            for pi in op.grad_params():
+                if pi not in seen:
+                    seen.add(pi)
+                    order.append(pi)
+        self.pgrad_order = order
+        self._eval_sig = None
+        self._eval_arena = None
+
+    def need_scratch(self, key, nbytes):
+        self.scratch_req[key] = max(self.scratch_req.get(key, 0), int(nbytes))
+
+    def params(self):
+        return [getattr(m, a) for (m, a) in self.param_refs]
+
+    # ------------------------------------------------------------------------------------
+    def ensure_eval_cache(self, device, stream):
+        """(Re)pack weights and fold BN when any parameter / buffer changed."""
+        sig = []
+        for op in self.ops:
+            if isinstance(op, ConvOp):
+                m = op.mod
+                for t in (m.conv.weight, m.bn.weight, m.bn.bias, m.bn.running_mean, m.bn.running_var):
+                    sig.append((t.data_ptr(), t._version))
+            elif isinstance(op, BiasConvOp):
+                sig.append((op.conv.weight.data_ptr(), op.conv.weight._version))
+        sig = tuple(sig)
+        if self._eval_arena is None or self._eval_arena.device != device:
+            self._eval_arena = torch.empty(max(self.eval_bytes, 1), dtype=torch.uint8, device=device)
+            self._eval_sig = None
+        if sig != self._eval_sig:
+            rt = Rt(self, None, stream, False)
+            rt.eval_base = self._eval_arena.data_ptr()
+            for op in self.ops:
+                if hasattr(op, "prepare_eval"):
+                    op.prepare_eval(rt)
+            self._eval_sig = sig
+        return self._eval_arena.data_ptr()
+
+    def new_arena(self, device, stream):
+        arena = torch.empty(max(self.arena_bytes, 1), dtype=torch.uint8, device=device)
+        base = arena.data_ptr()
+        for off, nb in self.zero_ranges:
+            L.call("yms_zero", base + off, nb, stream)
+        return arena
+
+    def act_tensor(self, arena, view, dtype):
+        """torch view (NCHW-shaped, channels-last strided) of an activation buffer slice."""
+        b = view.buf
+        nb = b.npix * b.ld * self.es
+        t = arena[b.off:b.off + nb].view(dtype).view(b.n, b.h, b.w, b.ld)
+        return t[..., view.off:view.off + view.c].permute(0, 3, 1, 2)

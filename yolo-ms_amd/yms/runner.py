@@ -1,0 +1,212 @@
+"""Module execution: plan cache, autograd bridge and dtype policy.
+
+``run(module, inputs)`` is what every yolov8 module's ``forward`` calls.  The whole
+module tree below it executes as ONE torch.autograd.Function whose forward/backward
+launch the plan's HIP kernels on the current stream; parameter gradients come back
+to autograd as views of a flat fp32 arena (so ``loss.backward(); opt.step()`` of the
+reference training loop, train.py:356-372, works unchanged).  There is no CPU or
+ATen-conv fallback: CPU tensors or a missing libyms.so raise RuntimeError.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from .plan import Builder, Plan, Rt
+
+_CACHE_ATTR = "_yms_plans"
+
+
+def compute_dtype(module):
+    """bf16/fp16 under torch.autocast('cuda'), else module.yms_dtype, else fp32."""
+    if torch.is_autocast_enabled("cuda"):
+        return torch.get_autocast_dtype("cuda")
+    return getattr(module, "yms_dtype", torch.float32)
+
+
+def set_compute_dtype(module, dtype):
+    """Run `module` (and its children when called through it) with bf16/fp16/fp32 kernels;
+    parameters stay fp32 masters."""
+    L.dtype_code(dtype)
+    for m in module.modules():
+        m.yms_dtype = dtype
+    return module
+
+
+class _State:
+    pass
+
+
+def _check_inputs(inputs):
+    for x in inputs:
+        if not isinstance(x, torch.Tensor) or x.device.type != "cuda":
+            raise RuntimeError("yms: the MI355X-native model runs on ROCm GPU tensors only "
+                               "(move the model and inputs to 'cuda'); there is no CPU fallback")
+
+
+def get_plan(module, inputs, dt, training):
+    key = (tuple(tuple(x.shape) for x in inputs), tuple(bool(x.requires_grad) for x in inputs), dt, training)
+    cache = module.__dict__.setdefault(_CACHE_ATTR, {})
+    plan = cache.get(key)
+    if plan is None:
+        for x in inputs:
+            if x.dim() != 4:
+                raise RuntimeError(f"yms: expected NCHW 4-D input, got shape {tuple(x.shape)}")
+        b = Builder(inputs[0].shape[0], L.dtype_code(dt), training)
+        in_views, outs, kind = module._yms_plan(b, inputs)
+        for v, x in zip(in_views, inputs):
+            v.buf.name = "input"
+            v.buf.needs_grad = bool(x.requires_grad)
+        plan = Plan(b, in_views, outs, kind)
+        cache[key] = plan
+    return plan
+
+
+def _load_inputs(plan, rt, inputs):
+    for x, v in zip(inputs, plan.inputs):
+        xc = x.contiguous()
+        if v.off == 0 and xc.dtype == torch.float32:
+            L.call("yms_pack_input", plan.dt, xc.shape[0], xc.shape[1], xc.shape[2], xc.shape[3], xc.data_ptr(),
+                   rt.a(v), v.buf.ld, rt.st)
+        else:
+            L.call("yms_nchw_to_nhwc", L.dtype_code(xc.dtype), plan.dt, xc.shape[0], xc.shape[2], xc.shape[3],
+                   xc.shape[1], xc.data_ptr(), rt.a(v), v.buf.ld, v.off, 0, rt.st)
+
+
+def _outputs(plan, arena, dtype):
+    return [plan.act_tensor(arena, v, dtype) for v in plan.outputs]
+
+
+def _decode(plan, rt, arena):
+    info = plan.kind[1].yms_decode_info()
+    n = plan.n
+    views = plan.outputs
+    nc = info["nc"]
+    A = sum(v.h * v.w for v in views)
+    out = torch.empty((n, A, 4 + nc), dtype=torch.float32, device=arena.device)
+    import ctypes
+    lv = (ctypes.c_void_p * 4)(*[rt.a(v) for v in views] + [None] * (4 - len(views)))
+    hs = (ctypes.c_int * 4)(*[v.h for v in views] + [0] * (4 - len(views)))
+    ws = (ctypes.c_int * 4)(*[v.w for v in views] + [0] * (4 - len(views)))
+    st = (ctypes.c_float * 4)(*(list(info["strides"]) + [0.0] * (4 - len(views))))
+    ld = views[0].buf.ld
+    for v in views:
+        if v.buf.ld != ld or v.off != 0:
+            raise RuntimeError("yms: head outputs must share one channel stride")
+    L.call("yms_head_decode", plan.dt, n, nc, len(views), lv, hs, ws, ld, st, out.data_ptr(),
+           ctypes.c_float(0.0), None, None, None, rt.st)
+    return out
+
+
+class _PlanFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, state, *args):
+        plan = state.plan
+        inputs = args[:len(plan.inputs)]
+        dev = inputs[0].device
+        stream = L.stream_ptr(dev)
+        arena = plan.new_arena(dev, stream)
+        rt = Rt(plan, arena.data_ptr(), stream, True)
+        _load_inputs(plan, rt, inputs)
+        for op in plan.ops:
+            op.fwd(rt)
+        state.arena = arena
+        state.rt = rt
+        state.in_meta = [(x.shape, x.dtype, x.requires_grad) for x in inputs]
+        state.used = False
+        ctx.state = state
+        outs = _outputs(plan, arena, state.dtype)
+        return tuple(outs)
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        state = ctx.state
+        if state.used:
+            raise RuntimeError("yms: backward through the same forward twice (retain_graph) is unsupported")
+        state.used = True
+        plan, rt = state.plan, state.rt
+        dev = state.arena.device
+        rt.st = L.stream_ptr(dev)
+        garena = torch.empty(max(plan.garena_bytes, 1), dtype=torch.uint8, device=dev)
+        rt.gbase = garena.data_ptr()
+        L.call("yms_zero", rt.gbase, plan.act_bytes, rt.st)
+        for v, g in zip(plan.outputs, gouts):
+            if g is None:
+                continue
+            gc = g.contiguous()
+            L.call("yms_nchw_to_nhwc", L.dtype_code(gc.dtype), plan.dt, gc.shape[0], gc.shape[2], gc.shape[3],
+                   gc.shape[1], gc.data_ptr(), rt.g(v), v.buf.ld, v.off, 1, rt.st)
+        params = state.params
+        need = [p.requires_grad for p in params]
+        total = sum(params[i].numel() for i in plan.pgrad_order if need[i])
+        pg = torch.empty(max(total, 1), dtype=torch.float32, device=dev)
+        ptrs = [None] * len(params)
+        views = [None] * len(params)
+        off = 0
+        for i in plan.pgrad_order:
+            if need[i]:
+                ptrs[i] = pg.data_ptr() + 4 * off
+                views[i] = pg[off:off + params[i].numel()].view(params[i].shape)
+                off += params[i].numel()
+        rt.pgrad = lambda i: ptrs[i]
+        hook = state.grad_hook
+        if hook is not None:
+            hook.begin(plan, pg, ptrs, views)
+        for op in reversed(plan.ops):
+            op.bwd(rt)
+            if hook is not None:
+                hook.op_done(op)
+        if hook is not None:
+            hook.finish()
+        in_grads = []
+        for (shape, dtype, rg), v in zip(state.in_meta, plan.inputs):
+            if rg:
+                gi = torch.empty(shape, dtype=dtype, device=dev)
+                L.call("yms_nhwc_to_nchw", plan.dt, L.dtype_code(dtype), shape[0], shape[2], shape[3], shape[1],
+                       rt.g(v), v.buf.ld, v.off, gi.data_ptr(), rt.st)
+                in_grads.append(gi)
+            else:
+                in_grads.append(None)
+        state.arena = None
+        return (None, *in_grads, *views)
+
+
+def run(module, inputs, grad_hook=None):
+    """Execute `module` on `inputs` (list of NCHW cuda tensors) through its plan."""
+    _check_inputs(inputs)
+    L.lib()
+    dtype = compute_dtype(module)
+    training = module.training
+    plan = get_plan(module, inputs, dtype, training)
+    params = plan.params()
+    dev = inputs[0].device
+    if training:
+        state = _State()
+        state.plan, state.dtype, state.params, state.grad_hook = plan, dtype, params, grad_hook
+        outs = _PlanFn.apply(state, *inputs, *params)
+        _bump_bn_counters(plan)
+        return plan, list(outs)
+    # eval / inference: no autograd graph, eval-cached packed weights + folded BN
+    stream = L.stream_ptr(dev)
+    with torch.no_grad():
+        arena = plan.new_arena(dev, stream)
+        rt = Rt(plan, arena.data_ptr(), stream, False)
+        rt.eval_base = plan.ensure_eval_cache(dev, stream)
+        _load_inputs(plan, rt, inputs)
+        for op in plan.ops:
+            op.fwd(rt)
+        if isinstance(plan.kind, tuple) and plan.kind[0] == "decode":
+            return plan, [_decode(plan, rt, arena)]
+        return plan, _outputs(plan, arena, dtype)
+
+
+def _bump_bn_counters(plan):
+    """nn.BatchNorm2d increments num_batches_tracked in training forward."""
+    ts = getattr(plan, "_nbt", None)
+    if ts is None:
+        from .plan import ConvOp
+        ts = [op.mod.bn.num_batches_tracked for op in plan.ops if isinstance(op, ConvOp)]
+        plan._nbt = ts
+    if ts:
+        with torch.no_grad():
+            torch._foreach_add_(ts, 1)
