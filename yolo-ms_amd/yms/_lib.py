@@ -106,8 +106,44 @@ def check(status, what):
         raise RuntimeError(f"yms: {what} failed: {msg} (status {status})")
 
 
+_prof = None
+_CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad")
+
+
 def call(name, *args):
+    if _prof is None:
+        check(getattr(lib(), name)(*args), name)
+        return
+    s = torch.cuda.Event(enable_timing=True)
+    e = torch.cuda.Event(enable_timing=True)
+    s.record()
     check(getattr(lib(), name)(*args), name)
+    e.record()
+    fl = 0
+    if name in _CONV:
+        sh = args[0].contents
+        fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
+    _prof.append((name, s, e, fl))
+
+
+def profile_begin():
+    """Record a HIP event pair around every C-ABI launch on the current stream (diagnostic)."""
+    global _prof
+    _prof = []
+
+
+def profile_end():
+    """-> {name: [calls, total_ms, flops]} for the launches since profile_begin()."""
+    global _prof
+    torch.cuda.synchronize()
+    out = {}
+    for name, s, e, fl in _prof:
+        r = out.setdefault(name, [0, 0.0, 0])
+        r[0] += 1
+        r[1] += s.elapsed_time(e)
+        r[2] += fl
+    _prof = None
+    return out
 
 
 def stream_ptr(device=None):

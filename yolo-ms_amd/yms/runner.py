@@ -175,6 +175,8 @@ def run(module, inputs, grad_hook=None):
     """Execute `module` on `inputs` (list of NCHW cuda tensors) through its plan."""
     _check_inputs(inputs)
     L.lib()
+    if grad_hook is None:
+        grad_hook = getattr(module, "_yms_grad_hook", None)
     dtype = compute_dtype(module)
     training = module.training
     plan = get_plan(module, inputs, dtype, training)
