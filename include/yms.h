@@ -106,7 +106,7 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
  *   reduce: partial sums of da and da*xhat (da = gy * silu'(a), a = z*scale+shift) -> ws
  *   finalize: dgamma, dbeta (+=) and the two per-channel coefficients
  *   apply: dz = scale*(da - mean(da) - xhat*mean(da*xhat)), written over dz (may alias z);
- *          gres (+)= gy when gres != NULL (residual branch). */
+ *          gres = gy (gres_acc=0) or gres += gy (gres_acc=1) when gres != NULL (residual). */
 int yms_bn_bwd_rows(long npix);
 yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
                                  const void* gy, int gy_ld, int gy_off, const float* scale,
@@ -118,7 +118,7 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
                                 const void* gy, int gy_ld, int gy_off, const float* scale,
                                 const float* shift, const float* mean_invstd, const float* coef,
                                 int act, void* dz, int dz_ld, int dz_off,
-                                void* gres, int gres_ld, int gres_off, void* stream);
+                                void* gres, int gres_ld, int gres_off, int gres_acc, void* stream);
 /* Bias-only backward of the head's 1x1 nn.Conv2d: dbias (+)= sum over pixels of gy. */
 yms_status yms_bias_bwd(int dtype, long npix, int c, const void* gy, int gy_ld, int gy_off,
                         float* ws, float* dbias, void* stream);
@@ -146,8 +146,9 @@ yms_status yms_nhwc_to_nchw(int dtype, int dtype_nchw, int n, int h, int w, int 
                             int ld, int off, void* y, void* stream);
 yms_status yms_nchw_to_nhwc(int dtype_nchw, int dtype, int n, int h, int w, int c, const void* x,
                             void* y, int ld, int off, int accumulate, void* stream);
-/* hipMemsetAsync(p, 0, bytes) on the stream. */
+/* hipMemsetAsync(p, 0, bytes) / device-to-device hipMemcpyAsync on the stream. */
 yms_status yms_zero(void* p, size_t bytes, void* stream);
+yms_status yms_copy(void* dst, const void* src, size_t bytes, void* stream);
 /* y = cast(x) elementwise (fp32 <-> dtype), count elements. */
 yms_status yms_cast(int dtype_in, int dtype_out, long count, const void* x, void* y, void* stream);
 

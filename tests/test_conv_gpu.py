@@ -21,6 +21,8 @@ SHAPES = [
     (3, 8, 17, 19, 130, 3, 1),
     (1, 1, 8, 8, 1, 3, 1),
     (2, 80, 11, 12, 80, 1, 1),
+    (2, 16, 9, 7, 24, 1, 2),        # 1x1 stride 2 (odd parity classes have no taps)
+    (1, 40, 15, 17, 48, 3, 2),      # odd sizes: unequal parity classes
 ]
 # bf16/f16 outputs are rounded to 8/11 significant bits; fp32 uses the exact-f32 MFMA
 TOL = {"f32": 2e-5, "bf16": 1e-2, "f16": 2e-3}

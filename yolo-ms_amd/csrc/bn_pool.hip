@@ -37,27 +37,36 @@ __global__ void bn_fold_kernel(int c, const float* g, const float* b, const floa
   shift[i] = b[i] - rm[i] * sc;
 }
 
-// stats: [rows][2][ld]; 32 channels x 8 row-lanes per block, fp64 accumulation.
-__global__ void bn_finalize_kernel(int c, const float* stats, int rows, int ld, long count,
-                                   const float* g, const float* b, float* rm, float* rv,
-                                   float momentum, float eps, float* mi, float* scale,
-                                   float* shift) {
-  __shared__ double red[2][8][33];
+// stats: [rows][2][ld]; 32 channels x 32 row-lanes per block (1024 threads), 4 independent
+// fp64 accumulators per lane so the row loop is load-throughput, not latency, bound.
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* stats, int rows, int ld,
+                                                           long count, const float* g, const float* b,
+                                                           float* rm, float* rv, float momentum, float eps,
+                                                           float* mi, float* scale, float* shift) {
+  __shared__ double red[2][32][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int ch = blockIdx.x * 32 + tx;
-  double s1 = 0.0, s2 = 0.0;
+  double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
   if (ch < c) {
-    for (int r = ty; r < rows; r += 8) {
-      s1 += stats[(long)r * 2 * ld + ch];
-      s2 += stats[(long)r * 2 * ld + ld + ch];
+    int r = ty;
+    for (; r + 96 < rows; r += 128) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a1[u] += stats[(long)(r + 32 * u) * 2 * ld + ch];
+        a2[u] += stats[(long)(r + 32 * u) * 2 * ld + ld + ch];
+      }
+    }
+    for (; r < rows; r += 32) {
+      a1[0] += stats[(long)r * 2 * ld + ch];
+      a2[0] += stats[(long)r * 2 * ld + ld + ch];
     }
   }
-  red[0][ty][tx] = s1;
-  red[1][ty][tx] = s2;
+  red[0][ty][tx] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+  red[1][ty][tx] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
   __syncthreads();
   if (ty == 0 && ch < c) {
     double t1 = 0.0, t2 = 0.0;
-    for (int k = 0; k < 8; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
+    for (int k = 0; k < 32; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
     const double mean = t1 / (double)count;
     double var = t2 / (double)count - mean * mean;
     if (var < 0.0) var = 0.0;
@@ -74,25 +83,48 @@ __global__ void bn_finalize_kernel(int c, const float* stats, int rows, int ld, 
 }
 
 // ------------------------------------------------------------------------------------------
-// y = act(z*scale + shift) (+ res)
+// Channel-stationary mapping for the per-channel elementwise / reduction kernels:
+// G = ceil(C/8) 16-B channel groups, thread (py, g) = (tid / G, tid % G) keeps the same
+// 8 channels (and their BN parameters, in registers) for every pixel it visits; the
+// PY = 256 / G pixel lanes of a block walk a contiguous pixel range.  One wave-row of a
+// pixel is a fully coalesced 16*G-byte segment.  Requires G <= 256 (C <= 2048).
 // ------------------------------------------------------------------------------------------
+struct ChanMap {
+  int G, PY, g, py;
+  bool active;
+  __device__ ChanMap(int c) {
+    G = (c + 7) >> 3;
+    PY = 256 / G;
+    g = threadIdx.x % G;
+    py = threadIdx.x / G;
+    active = py < PY;
+  }
+};
+
+__device__ __forceinline__ void load_params8(const float* p, int c0, int c, float (&v)[8], float dflt) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) v[i] = (p && c0 + i < c) ? p[c0 + i] : dflt;
+}
+
 template <typename T>
-__global__ void affine_act_kernel(long npix, int c, const T* z, int z_ld, int z_off,
-                                  const float* scale, const float* shift, int act, const T* res,
-                                  int res_ld, int res_off, T* y, int y_ld, int y_off) {
-  const int G = (c + 7) >> 3;
-  const long total = npix * G;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long pix = t / G;
-    const int g = (int)(t - pix * G);
-    const int c0 = g * 8, nv = min(8, c - c0);
+__global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const T* z, int z_ld, int z_off,
+                                                         const float* scale, const float* shift, int act,
+                                                         const T* res, int res_ld, int res_off, T* y,
+                                                         int y_ld, int y_off, long ppb) {
+  ChanMap m(c);
+  if (!m.active) return;
+  const int c0 = m.g * 8, nv = min(8, c - c0);
+  float sc[8], sh[8];
+  load_params8(scale, c0, c, sc, 1.0f);
+  load_params8(shift, c0, c, sh, 0.0f);
+  const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
+  for (long pix = p0 + m.py; pix < p1; pix += m.PY) {
     float v[8], r[8];
     load8(z + pix * z_ld + z_off + c0, nv, v);
     if (res) load8(res + pix * res_ld + res_off + c0, nv, r);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int ch = min(c0 + i, c - 1);
-      float a = v[i] * (scale ? scale[ch] : 1.0f) + (shift ? shift[ch] : 0.0f);
+      float a = v[i] * sc[i] + sh[i];
       if (act == YMS_ACT_SILU) a = silu_f(a);
       if (res) a += r[i];
       v[i] = a;
@@ -102,96 +134,102 @@ __global__ void affine_act_kernel(long npix, int c, const T* z, int z_ld, int z_
 }
 
 // ------------------------------------------------------------------------------------------
-// BN + SiLU backward.  Block = 32 channel-group lanes x 8 pixel lanes; each block owns a
-// contiguous pixel range and writes one partial row [2][c] (deterministic).
+// BN + SiLU backward.  Each block owns a contiguous pixel range and writes one partial row
+// [2][c] (sum da, sum da*xhat) -- deterministic, no atomics.
 // ------------------------------------------------------------------------------------------
-constexpr int BWD_NG = 4;   // channel groups (of 8) per thread lane -> up to 1024 channels
-
 template <typename T, bool HAS_Z>
-__global__ void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld, int z_off,
-                                     const T* gy, int gy_ld, int gy_off, const float* scale,
-                                     const float* shift, const float* mi, int act, float* ws,
-                                     long pix_per_block) {
-  __shared__ float red[8][2][256 + 8];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int G = (c + 7) >> 3;
-  const long p0 = blockIdx.x * pix_per_block;
-  const long p1 = min(npix, p0 + pix_per_block);
-  for (int gbase = 0; gbase < G; gbase += 32 * BWD_NG) {
-    float acc1[BWD_NG][8], acc2[BWD_NG][8];
+__global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld,
+                                                            int z_off, const T* gy, int gy_ld, int gy_off,
+                                                            const float* scale, const float* shift,
+                                                            const float* mi, int act, float* ws, long ppb) {
+  __shared__ float red[2][2048 + 64];
+  ChanMap m(c);
+  const int c0 = m.g * 8, nv = min(8, c - c0);
+  float a1[8], a2[8];
 #pragma unroll
-    for (int k = 0; k < BWD_NG; ++k)
-#pragma unroll
-      for (int i = 0; i < 8; ++i) { acc1[k][i] = 0.f; acc2[k][i] = 0.f; }
-    for (long pix = p0 + ty; pix < p1; pix += 8) {
-#pragma unroll
-      for (int k = 0; k < BWD_NG; ++k) {
-        const int g = gbase + tx + 32 * k;
-        if (g >= G) continue;
-        const int c0 = g * 8, nv = min(8, c - c0);
-        float gv[8], zv[8];
-        load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
-        if (HAS_Z) load8(z + pix * z_ld + z_off + c0, nv, zv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          const int ch = min(c0 + i, c - 1);
-          float da = gv[i], xh = 0.f;
-          if (HAS_Z) {
-            const float a = zv[i] * scale[ch] + shift[ch];
-            if (act == YMS_ACT_SILU) {
-              const float s = sigmoid_f(a);
-              da = gv[i] * (s * (1.0f + a * (1.0f - s)));
-            }
-            xh = (zv[i] - mi[ch]) * mi[c + ch];
-          }
-          acc1[k][i] += da;
-          acc2[k][i] += da * xh;
-        }
-      }
+  for (int i = 0; i < 8; ++i) { a1[i] = 0.f; a2[i] = 0.f; }
+  if (m.active) {
+    float sc[8], sh[8], mu[8], is[8];
+    if (HAS_Z) {
+      load_params8(scale, c0, c, sc, 0.f);
+      load_params8(shift, c0, c, sh, 0.f);
+      load_params8(mi, c0, c, mu, 0.f);
+      load_params8(mi + c, c0, c, is, 0.f);
     }
-    // reduce over the 8 pixel lanes (fixed order), one channel-group chunk at a time
-#pragma unroll
-    for (int k = 0; k < BWD_NG; ++k) {
-      const int g = gbase + tx + 32 * k;
+    const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
+    for (long pix = p0 + m.py; pix < p1; pix += m.PY) {
+      float gv[8], zv[8];
+      load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
+      if (HAS_Z) load8(z + pix * z_ld + z_off + c0, nv, zv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) {
-        red[ty][0][tx * 8 + i] = acc1[k][i];
-        red[ty][1][tx * 8 + i] = acc2[k][i];
+        float da = gv[i], xh = 0.f;
+        if (HAS_Z) {
+          const float a = zv[i] * sc[i] + sh[i];
+          if (act == YMS_ACT_SILU) {
+            const float s = sigmoid_f(a);
+            da = gv[i] * (s * (1.0f + a * (1.0f - s)));
+          }
+          xh = (zv[i] - mu[i]) * is[i];
+        }
+        a1[i] += da;
+        a2[i] += da * xh;
       }
-      __syncthreads();
-      // 256 threads finalize 256 channels of this chunk
-      const int cl = threadIdx.x;  // local channel in [0, 256)
-      const int ch = (gbase + 32 * k) * 8 + cl;
-      float t1 = 0.f, t2 = 0.f;
+    }
+  }
+  // reduce over the PY pixel lanes in a fixed order: red[k][py*8G + g*8 + i]
+  const int W = m.G * 8;
+  for (int lane0 = 0; lane0 < m.PY; lane0 += 2048 / W) {
+    const int lanes = min(m.PY - lane0, 2048 / W);
+    if (m.active && m.py >= lane0 && m.py < lane0 + lanes) {
 #pragma unroll
-      for (int w = 0; w < 8; ++w) { t1 += red[w][0][cl]; t2 += red[w][1][cl]; }
-      if (ch < c) {
+      for (int i = 0; i < 8; ++i) {
+        red[0][(m.py - lane0) * W + c0 + i] = a1[i];
+        red[1][(m.py - lane0) * W + c0 + i] = a2[i];
+      }
+    }
+    __syncthreads();
+    for (int ch = threadIdx.x; ch < c; ch += 256) {
+      float t1 = 0.f, t2 = 0.f;
+      for (int l = 0; l < lanes; ++l) { t1 += red[0][l * W + ch]; t2 += red[1][l * W + ch]; }
+      if (lane0 == 0) {
         ws[(long)blockIdx.x * 2 * c + ch] = t1;
         ws[(long)blockIdx.x * 2 * c + c + ch] = t2;
+      } else {
+        ws[(long)blockIdx.x * 2 * c + ch] += t1;
+        ws[(long)blockIdx.x * 2 * c + c + ch] += t2;
       }
-      __syncthreads();
-      (void)g;
     }
+    __syncthreads();
   }
 }
 
-__global__ void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long count, float* dgamma,
-                                       float* dbeta, float* coef) {
-  __shared__ double red[2][8][33];
+__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long count,
+                                                               float* dgamma, float* dbeta, float* coef) {
+  __shared__ double red[2][32][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int ch = blockIdx.x * 32 + tx;
-  double s1 = 0.0, s2 = 0.0;
-  if (ch < c)
-    for (int r = ty; r < rows; r += 8) {
-      s1 += ws[(long)r * 2 * c + ch];
-      s2 += ws[(long)r * 2 * c + c + ch];
+  double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
+  if (ch < c) {
+    int r = ty;
+    for (; r + 96 < rows; r += 128) {
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        a1[u] += ws[(long)(r + 32 * u) * 2 * c + ch];
+        a2[u] += ws[(long)(r + 32 * u) * 2 * c + c + ch];
+      }
     }
-  red[0][ty][tx] = s1;
-  red[1][ty][tx] = s2;
+    for (; r < rows; r += 32) {
+      a1[0] += ws[(long)r * 2 * c + ch];
+      a2[0] += ws[(long)r * 2 * c + c + ch];
+    }
+  }
+  red[0][ty][tx] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+  red[1][ty][tx] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
   __syncthreads();
   if (ty == 0 && ch < c) {
     double t1 = 0.0, t2 = 0.0;
-    for (int k = 0; k < 8; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
+    for (int k = 0; k < 32; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
     if (dbeta) dbeta[ch] = (float)t1;
     if (dgamma) dgamma[ch] = (float)t2;
     if (coef) {
@@ -202,36 +240,48 @@ __global__ void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long co
 }
 
 template <typename T>
-__global__ void bn_bwd_apply_kernel(long npix, int c, const T* z, int z_ld, int z_off, const T* gy,
-                                    int gy_ld, int gy_off, const float* scale, const float* shift,
-                                    const float* mi, const float* coef, int act, T* dz, int dz_ld,
-                                    int dz_off, T* gres, int gres_ld, int gres_off) {
-  const int G = (c + 7) >> 3;
-  const long total = npix * G;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const long pix = t / G;
-    const int g = (int)(t - pix * G);
-    const int c0 = g * 8, nv = min(8, c - c0);
+__global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, const T* z, int z_ld, int z_off,
+                                                           const T* gy, int gy_ld, int gy_off, const float* scale,
+                                                           const float* shift, const float* mi,
+                                                           const float* coef, int act, T* dz, int dz_ld,
+                                                           int dz_off, T* gres, int gres_ld, int gres_off,
+                                                           int gres_acc, long ppb) {
+  ChanMap m(c);
+  if (!m.active) return;
+  const int c0 = m.g * 8, nv = min(8, c - c0);
+  float sc[8], sh[8], mu[8], is[8], k0[8], k1[8];
+  load_params8(scale, c0, c, sc, 0.f);
+  load_params8(shift, c0, c, sh, 0.f);
+  load_params8(mi, c0, c, mu, 0.f);
+  load_params8(mi + c, c0, c, is, 0.f);
+  load_params8(coef, c0, c, k0, 0.f);
+  load_params8(coef + c, c0, c, k1, 0.f);
+  const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
+  for (long pix = p0 + m.py; pix < p1; pix += m.PY) {
     float gv[8], zv[8], out[8];
     load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
     load8(z + pix * z_ld + z_off + c0, nv, zv);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int ch = min(c0 + i, c - 1);
-      const float a = zv[i] * scale[ch] + shift[ch];
+      const float a = zv[i] * sc[i] + sh[i];
       float da = gv[i];
       if (act == YMS_ACT_SILU) {
         const float s = sigmoid_f(a);
         da = gv[i] * (s * (1.0f + a * (1.0f - s)));
       }
-      const float xh = (zv[i] - mi[ch]) * mi[c + ch];
-      out[i] = scale[ch] * (da - coef[ch] - xh * coef[c + ch]);
+      const float xh = (zv[i] - mu[i]) * is[i];
+      out[i] = sc[i] * (da - k0[i] - xh * k1[i]);
     }
     if (gres) {
       float r[8];
-      load8(gres + pix * gres_ld + gres_off + c0, nv, r);
+      if (gres_acc) {
+        load8(gres + pix * gres_ld + gres_off + c0, nv, r);
 #pragma unroll
-      for (int i = 0; i < 8; ++i) r[i] += gv[i];
+        for (int i = 0; i < 8; ++i) r[i] += gv[i];
+      } else {
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = gv[i];
+      }
       store8(gres + pix * gres_ld + gres_off + c0, nv, r);
     }
     store8(dz + pix * dz_ld + dz_off + c0, nv, out);
@@ -520,10 +570,15 @@ yms_status yms_bn_finalize(int c, const float* stats, int rows, int stats_ld, lo
                            float* shift, void* stream) {
   if (c <= 0 || !stats || rows <= 0 || count <= 0 || !gamma || !beta || !mean_invstd || !scale || !shift)
     return YMS_ERR_INVALID;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, stats,
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, stats,
                      rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps, mean_invstd, scale,
                      shift);
   return launch_status();
+}
+
+static long elem_ppb(long npix) {
+  const long blocks = std::min<long>(std::max<long>((npix + 63) / 64, 1), 4096);
+  return (npix + blocks - 1) / blocks;
 }
 
 yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
@@ -532,18 +587,20 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
                           void* y, int y_ld, int y_off, void* stream) {
   if (npix <= 0 || !z || !y || !vok(z_ld, z_off, c) || !vok(y_ld, y_off, c)) return YMS_ERR_INVALID;
   if (res && !vok(res_ld, res_off, c)) return YMS_ERR_INVALID;
-  const long items = npix * ((c + 7) / 8);
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(affine_act_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+  if (c > 2048) return YMS_ERR_UNSUPPORTED;
+  const long ppb = elem_ppb(npix);
+  const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(affine_act_kernel<T>, dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
                                                scale, shift, act, (const T*)res, res_ld, res_off, (T*)y,
-                                               y_ld, y_off));
+                                               y_ld, y_off, ppb));
   return launch_status();
 }
 
 int yms_bn_bwd_rows(long npix) {
   if (npix <= 0) return 0;
   long rows = (npix + 255) / 256;
-  if (rows > 2048) rows = 2048;
+  if (rows > 1024) rows = 1024;
   return (int)rows;
 }
 
@@ -558,6 +615,7 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
                                  float* ws, void* stream) {
   if (npix <= 0 || !gy || !ws || !vok(gy_ld, gy_off, c)) return YMS_ERR_INVALID;
   if (z && (!vok(z_ld, z_off, c) || !scale || !shift || !mean_invstd)) return YMS_ERR_INVALID;
+  if (c > 2048) return YMS_ERR_UNSUPPORTED;
   const long ppb = bwd_pix_per_block(npix);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
   if (z) {
@@ -577,7 +635,7 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
 yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count, float* dgamma,
                                    float* dbeta, float* coef, void* stream) {
   if (c <= 0 || !ws || rows <= 0 || count <= 0) return YMS_ERR_INVALID;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, ws,
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, ws,
                      rows, count, dgamma, dbeta, coef);
   return launch_status();
 }
@@ -586,15 +644,17 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
                                 const void* gy, int gy_ld, int gy_off, const float* scale,
                                 const float* shift, const float* mean_invstd, const float* coef,
                                 int act, void* dz, int dz_ld, int dz_off,
-                                void* gres, int gres_ld, int gres_off, void* stream) {
+                                void* gres, int gres_ld, int gres_off, int gres_acc, void* stream) {
   if (npix <= 0 || !z || !gy || !dz || !scale || !shift || !mean_invstd || !coef) return YMS_ERR_INVALID;
   if (!vok(z_ld, z_off, c) || !vok(gy_ld, gy_off, c) || !vok(dz_ld, dz_off, c)) return YMS_ERR_INVALID;
   if (gres && !vok(gres_ld, gres_off, c)) return YMS_ERR_INVALID;
-  const long items = npix * ((c + 7) / 8);
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+  if (c > 2048) return YMS_ERR_UNSUPPORTED;
+  const long ppb = elem_ppb(npix);
+  const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
                                                (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd, coef,
-                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off));
+                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off, gres_acc, ppb));
   return launch_status();
 }
 
@@ -707,4 +767,11 @@ extern "C" yms_status yms_zero(void* p, size_t bytes, void* stream) {
   if (!p) return YMS_ERR_INVALID;
   if (bytes == 0) return YMS_OK;
   return hipMemsetAsync(p, 0, bytes, (hipStream_t)stream) == hipSuccess ? YMS_OK : YMS_ERR_LAUNCH;
+}
+
+extern "C" yms_status yms_copy(void* dst, const void* src, size_t bytes, void* stream) {
+  if (!dst || !src) return YMS_ERR_INVALID;
+  if (bytes == 0) return YMS_OK;
+  return hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToDevice, (hipStream_t)stream) == hipSuccess
+             ? YMS_OK : YMS_ERR_LAUNCH;
 }

@@ -22,7 +22,7 @@ namespace yms {
 
 constexpr int NT_ROWP = 80;  // bytes per LDS row (64 B of K + 16 B pad)
 
-enum { MODE_FWD = 0, MODE_DGRAD = 1 };
+enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD2 = 2 };  // DGRAD2: stride-2 dgrad by output parity
 enum { EPI_AFFINE = 0, EPI_STATS = 1, EPI_STORE = 2, EPI_ACCUM = 3 };
 
 struct NTParams {
@@ -47,6 +47,13 @@ struct NTParams {
   int Ncols;        // valid output columns
   int tiles_n;
   FastDiv div_ow, div_ohw;
+  // MODE_DGRAD2: one GEMM per output-parity class (ry, rx) = (blockIdx.y >> 1, blockIdx.y & 1).
+  // Class rows are the dx pixels (n, 2a+ry, 2b+rx); its taps are kh = kh0 + 2*jy, kw = kw0 + 2*jx,
+  // reading dz at (a + c0y - jy, b + c0x - jx); weights are packed per class.
+  int OH, OWx;                      // dx spatial dims (for the output pixel index)
+  int cls_M[4], cls_nkt[4], cls_Kc[4], cls_ntx[4], cls_c0y[4], cls_c0x[4];
+  long cls_woff[4];                 // byte offset of the class' packed weight block
+  FastDiv cls_div_w[4], cls_div_hw[4];
 };
 
 template <typename T> struct Mfma;
@@ -84,6 +91,20 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
   const int wm = wave / WGN, wn = wave % WGN;
   const int tile_n = blockIdx.x % p.tiles_n, tile_m = blockIdx.x / p.tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
+  int M = p.M, nkt = p.nkt, Kc = p.Kc, ntx = 1, cls = 0;
+  const char* wp = p.wp;
+  FastDiv dv_w = p.div_ow, dv_hw = p.div_ohw;
+  if (MODE == MODE_DGRAD2) {
+    cls = blockIdx.y;
+    M = p.cls_M[cls];
+    nkt = p.cls_nkt[cls];
+    Kc = p.cls_Kc[cls];
+    ntx = p.cls_ntx[cls];
+    wp = p.wp + p.cls_woff[cls];
+    dv_w = p.cls_div_w[cls];
+    dv_hw = p.cls_div_hw[cls];
+    if (m0 >= M) return;   // uniform: this class has fewer row tiles
+  }
 
   // ---- im2col loader state (A side): fixed chunk column q, rows r0 + 64*i ----
   const int q = tid & 3, r0 = tid >> 2;
@@ -92,19 +113,22 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
 #pragma unroll
   for (int i = 0; i < A_SLOTS; ++i) {
     const int m = m0 + r0 + 64 * i;
-    a_ok[i] = m < p.M;
+    a_ok[i] = m < M;
     const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
-    const uint32_t n = fdiv(mm, p.div_ohw);
-    const uint32_t rem = mm - n * p.div_ohw.d;
-    const uint32_t oy = fdiv(rem, p.div_ow);
-    const uint32_t ox = rem - oy * p.div_ow.d;
+    const uint32_t n = fdiv(mm, dv_hw);
+    const uint32_t rem = mm - n * dv_hw.d;
+    const uint32_t oy = fdiv(rem, dv_w);
+    const uint32_t ox = rem - oy * dv_w.d;
     a_base[i] = (int)n * p.SH;
     if (MODE == MODE_FWD) {
       a_y[i] = (int)oy * p.stride - p.pad;
       a_x[i] = (int)ox * p.stride - p.pad;
-    } else {
+    } else if (MODE == MODE_DGRAD) {
       a_y[i] = (int)oy + p.pad;
       a_x[i] = (int)ox + p.pad;
+    } else {
+      a_y[i] = (int)oy + p.cls_c0y[cls];
+      a_x[i] = (int)ox + p.cls_c0x[cls];
     }
   }
   int tap = q / p.cpt, cc = q - (q / p.cpt) * p.cpt;
@@ -113,8 +137,15 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
 
   auto load_tile = [&](int kt) {
     const int kc = kt * 4 + q;
-    const int kh = tap / KS, kw = tap - (tap / KS) * KS;
-    const bool kok = kc < p.Kc;
+    int kh, kw;
+    if (MODE == MODE_DGRAD2) {
+      kh = ntx == 1 ? tap : (tap >> 1);     // jy
+      kw = ntx == 1 ? 0 : (tap & 1);        // jx
+    } else {
+      kh = tap / KS;
+      kw = tap - (tap / KS) * KS;
+    }
+    const bool kok = kc < Kc;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
       int iy, ix;
@@ -122,6 +153,9 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
       if (MODE == MODE_FWD) {
         iy = a_y[i] + kh;
         ix = a_x[i] + kw;
+      } else if (MODE == MODE_DGRAD2) {
+        iy = a_y[i] - kh;
+        ix = a_x[i] - kw;
       } else {
         const int ty = a_y[i] - kh, tx = a_x[i] - kw;
         if (p.stride == 2) {
@@ -146,8 +180,8 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
       const int c = tid + 256 * j;
       if (c < B_CHUNKS) {
         const int row = c >> 2, qq = c & 3;
-        const long off = ((long)(n0 + row) * (p.nkt * 4) + kt * 4 + qq) * 16;
-        b_reg[j] = *reinterpret_cast<const uint4*>(p.wp + off);
+        const long off = ((long)(n0 + row) * (nkt * 4) + kt * 4 + qq) * 16;
+        b_reg[j] = *reinterpret_cast<const uint4*>(wp + off);
       }
     }
     // advance the tap cursor by 4 chunks for the next k-tile
@@ -226,9 +260,9 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
   load_tile(0);
   store_tile(0);
   __syncthreads();
-  for (int kt = 0; kt < p.nkt; ++kt) {
+  for (int kt = 0; kt < nkt; ++kt) {
     const int cur = kt & 1;
-    const bool more = kt + 1 < p.nkt;
+    const bool more = kt + 1 < nkt;
     if (more) load_tile(kt + 1);
     compute(cur);
     if (more) store_tile(cur ^ 1);
@@ -252,13 +286,21 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
     for (int a = 0; a < TM; ++a) {
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        const int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
         float v = acc[a][b][i];
         if (EPI == EPI_STATS) {
           s1[b] += v;
           s2[b] += v * v;
         }
-        if (row < p.M && col_ok) {
+        const bool row_ok = row < M;
+        if (MODE == MODE_DGRAD2 && row_ok) {
+          const uint32_t n = fdiv((uint32_t)row, dv_hw);
+          const uint32_t rem = (uint32_t)row - n * dv_hw.d;
+          const uint32_t ya = fdiv(rem, dv_w);
+          const uint32_t xb = rem - ya * dv_w.d;
+          row = ((int)n * p.OH + 2 * (int)ya + (cls >> 1)) * p.OWx + 2 * (int)xb + (cls & 1);
+        }
+        if (row_ok && col_ok) {
           if (EPI == EPI_AFFINE) {
             v = v * sc + sh;
             if (p.act == YMS_ACT_SILU) v = silu_f(v);
@@ -496,21 +538,53 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
       }
 }
 
-// dw[co][ci][kh][kw] (+)= sum_s slab[s][co][tap*cin8 + ci]; threads walk the slab order.
-__global__ void wgrad_reduce_kernel(const float* slab, int splits, long slab_elems, int slab_ld,
-                                    int cout, int cin, int cin8, int ks, float* dw, int accumulate) {
-  const long total = (long)cout * ks * ks * cin8;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int ci = (int)(t % cin8);
-    const long r = t / cin8;
-    const int tap = (int)(r % (ks * ks));
-    const int co = (int)(r / (ks * ks));
-    if (ci >= cin) continue;
-    const long sidx = (long)co * slab_ld + (long)tap * cin8 + ci;
-    float s = 0.f;
-    for (int z = 0; z < splits; ++z) s += slab[z * slab_elems + sidx];
-    const long o = (((long)co * cin + ci) * ks + tap / ks) * ks + tap % ks;
-    dw[o] = accumulate ? dw[o] + s : s;
+// dw[co][ci][kh][kw] (+)= sum_s slab[s][co][tap*cin8 + ci].  Block = 32 float4 lanes (128
+// consecutive slab columns of one row) x 8 split lanes; every lane keeps two independent
+// float4 accumulators, the 8 split lanes are combined through LDS in a fixed order
+// (deterministic).  Reads are 16 B/lane, fully coalesced along the slab row.
+__global__ __launch_bounds__(256) void wgrad_reduce_kernel(const float* slab, int splits, long slab_elems,
+                                                           int slab_ld, int cout, int cin, int cin8, int ks,
+                                                           float* dw, int accumulate) {
+  __shared__ float4 red[8][33];
+  const int lx = threadIdx.x & 31, ly = threadIdx.x >> 5;
+  const int kf = ks * ks * cin8;                // valid slab columns
+  const int cpr = (kf + 127) / 128;             // column blocks per row
+  const int co = blockIdx.x / cpr;
+  const int col = (blockIdx.x - co * cpr) * 128 + lx * 4;
+  float4 a = make_float4(0.f, 0.f, 0.f, 0.f), b = a;
+  if (col < kf) {
+    const float* base = slab + (long)co * slab_ld + col;
+    int z = ly;
+    for (; z + 8 < splits; z += 16) {
+      const float4 u = *reinterpret_cast<const float4*>(base + (long)z * slab_elems);
+      const float4 v = *reinterpret_cast<const float4*>(base + (long)(z + 8) * slab_elems);
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+      b.x += v.x; b.y += v.y; b.z += v.z; b.w += v.w;
+    }
+    if (z < splits) {
+      const float4 u = *reinterpret_cast<const float4*>(base + (long)z * slab_elems);
+      a.x += u.x; a.y += u.y; a.z += u.z; a.w += u.w;
+    }
+  }
+  red[ly][lx] = make_float4(a.x + b.x, a.y + b.y, a.z + b.z, a.w + b.w);
+  __syncthreads();
+  if (ly == 0 && col < kf) {
+    float4 t = red[0][lx];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float4 u = red[k][lx];
+      t.x += u.x; t.y += u.y; t.z += u.z; t.w += u.w;
+    }
+    const float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = col + e;
+      const int tap = c / cin8, ci = c - tap * cin8;
+      if (ci < cin) {
+        const long o = (((long)co * cin + ci) * ks + tap / ks) * ks + tap % ks;
+        dw[o] = accumulate ? dw[o] + tv[e] : tv[e];
+      }
+    }
   }
 }
 
@@ -537,6 +611,31 @@ __global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, in
   }
 }
 
+// stride-2 dgrad: 4 parity-class blocks, block c = [cin_pad128][kp_c]; K = (jy, jx, co8)
+struct Dg2Pack {
+  long off[4];       // element offset of each class block
+  int kp[4];         // elements per row of each class block
+  int ntx[4], kh0[4], kw0[4];
+};
+template <typename T>
+__global__ void pack_weight_dgrad2_kernel(const float* w, T* out, int cout, int cin, int ks, int rows, int c8,
+                                          Dg2Pack g, long total) {
+  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+    int c = 0;
+    while (c < 3 && t >= g.off[c + 1]) ++c;
+    const long e = t - g.off[c];
+    const int r = (int)(e / g.kp[c]);       // ci
+    const int k = (int)(e % g.kp[c]);
+    const int tl = k / c8, co = k % c8;
+    const int jy = tl / g.ntx[c], jx = tl % g.ntx[c];
+    const int kh = g.kh0[c] + 2 * jy, kw = g.kw0[c] + 2 * jx;
+    float v = 0.f;
+    if (kh < ks && kw < ks && co < cout && r < cin) v = w[((long)co * cin + r) * ks * ks + kh * ks + kw];
+    out[t] = (T)v;
+  }
+  (void)rows;
+}
+
 // ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
@@ -556,6 +655,38 @@ static PackGeo pack_geo(const yms_conv_shape* s, int for_dgrad) {
   g.nkt = cdiv(g.kc, 4);
   g.kp_elems = g.nkt * 64 / es;
   g.rows = (int)rup(cout_r, 128);
+  return g;
+}
+
+struct Dg2Geo {
+  int M[4], nkt[4], Kc[4], ntx[4], nty[4], c0y[4], c0x[4], kh0[4], kw0[4], Ha[4], Wa[4], kp[4];
+  long off_elems[5];
+  int rows, cpt;
+};
+static Dg2Geo dg2_geo(const yms_conv_shape* s) {
+  Dg2Geo g;
+  const int es = elem_size(s->dtype);
+  const int c8 = (int)rup(s->cout, 8);
+  g.cpt = c8 * es / 16;
+  g.rows = (int)rup(s->cin, 128);
+  g.off_elems[0] = 0;
+  for (int c = 0; c < 4; ++c) {
+    const int ry = c >> 1, rx = c & 1;
+    const int kh0 = (ry + s->pad) & 1, kw0 = (rx + s->pad) & 1;
+    g.kh0[c] = kh0;
+    g.kw0[c] = kw0;
+    g.nty[c] = (s->k - kh0 + 1) / 2;
+    g.ntx[c] = (s->k - kw0 + 1) / 2;
+    g.c0y[c] = (ry + s->pad - kh0) / 2;
+    g.c0x[c] = (rx + s->pad - kw0) / 2;
+    g.Ha[c] = (s->h - ry + 1) / 2;
+    g.Wa[c] = (s->w - rx + 1) / 2;
+    g.M[c] = s->n * g.Ha[c] * g.Wa[c];
+    g.Kc[c] = g.nty[c] * g.ntx[c] * g.cpt;
+    g.nkt[c] = std::max(1, cdiv(g.Kc[c], 4));
+    g.kp[c] = g.nkt[c] * 64 / es;
+    g.off_elems[c + 1] = g.off_elems[c] + (long)g.rows * g.kp[c];
+  }
   return g;
 }
 
@@ -586,17 +717,18 @@ static TileChoice choose_tile(int ncols) {
 template <typename T, int KS, int MODE, int EPI>
 static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
   NTParams p = p0;
+  const unsigned gy = MODE == MODE_DGRAD2 ? 4u : 1u;
   if (cfg == 0) {
     p.tiles_n = cdiv(p.Ncols, 128);
-    dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n));
+    dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
     hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 128, 2, 2>), grid, dim3(256), 0, st, p);
   } else if (cfg == 1) {
     p.tiles_n = cdiv(p.Ncols, 64);
-    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n));
+    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n), gy);
     hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 256, 64, 4, 1>), grid, dim3(256), 0, st, p);
   } else {
     p.tiles_n = cdiv(p.Ncols, 32);
-    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n));
+    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n), gy);
     hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 256, 32, 4, 1>), grid, dim3(256), 0, st, p);
   }
 }
@@ -604,7 +736,8 @@ static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
 template <int MODE, int EPI>
 static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hipStream_t st) {
 #define YMS_NT_CASE(T)                                          \
-  if (ks == 1) launch_nt<T, 1, MODE, EPI>(p, cfg, st);          \
+  if constexpr (MODE == MODE_DGRAD2) launch_nt<T, 3, MODE, EPI>(p, cfg, st);   \
+  else if (ks == 1) launch_nt<T, 1, MODE, EPI>(p, cfg, st);     \
   else launch_nt<T, 3, MODE, EPI>(p, cfg, st);
   if (dtype == YMS_BF16) { YMS_NT_CASE(bf16) }
   else if (dtype == YMS_F16) { YMS_NT_CASE(f16) }
@@ -634,7 +767,8 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   const long M = (long)s->n * s->ho * s->wo;
   w.nkt = cdiv(M, 32);
   const int blocks = w.tiles_m * w.tiles_n;
-  int splits = std::max(1, std::min(w.nkt, cdiv(2048, blocks)));
+  // ~1024 GEMM workgroups in flight, but at least 16 pixel tiles (512 pixels) per split
+  int splits = std::max(1, std::min(cdiv(w.nkt, 16), cdiv(1024, blocks)));
   w.kt_per_split = cdiv(w.nkt, splits);
   w.splits = cdiv(w.nkt, w.kt_per_split);
   return w;
@@ -656,6 +790,7 @@ extern "C" {
 
 size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad) {
   if (!shape_ok(s)) return 0;
+  if (for_dgrad && s->stride == 2) return (size_t)dg2_geo(s).off_elems[4];
   PackGeo g = pack_geo(s, for_dgrad);
   return (size_t)g.rows * g.kp_elems;
 }
@@ -663,8 +798,29 @@ size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad) {
 yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* packed,
                                 int for_dgrad, void* stream) {
   if (!shape_ok(s) || !w || !packed) return YMS_ERR_INVALID;
-  PackGeo g = pack_geo(s, for_dgrad);
   hipStream_t st = (hipStream_t)stream;
+  if (for_dgrad && s->stride == 2) {
+    Dg2Geo d = dg2_geo(s);
+    Dg2Pack pk;
+    for (int c = 0; c < 4; ++c) {
+      pk.off[c] = d.off_elems[c];
+      pk.kp[c] = d.kp[c];
+      pk.ntx[c] = d.ntx[c];
+      pk.kh0[c] = d.kh0[c];
+      pk.kw0[c] = d.kw0[c];
+    }
+    const long total = d.off_elems[4];
+    const int c8 = (int)rup(s->cout, 8);
+    dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 4096));
+    if (s->dtype == YMS_BF16)
+      hipLaunchKernelGGL(pack_weight_dgrad2_kernel<bf16>, grid, dim3(256), 0, st, w, (bf16*)packed, s->cout, s->cin, s->k, d.rows, c8, pk, total);
+    else if (s->dtype == YMS_F16)
+      hipLaunchKernelGGL(pack_weight_dgrad2_kernel<f16>, grid, dim3(256), 0, st, w, (f16*)packed, s->cout, s->cin, s->k, d.rows, c8, pk, total);
+    else
+      hipLaunchKernelGGL(pack_weight_dgrad2_kernel<float>, grid, dim3(256), 0, st, w, (float*)packed, s->cout, s->cin, s->k, d.rows, c8, pk, total);
+    return launch_status();
+  }
+  PackGeo g = pack_geo(s, for_dgrad);
   const long total = (long)g.rows * g.kp_elems;
   dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 4096));
   if (s->dtype == YMS_BF16)
@@ -723,7 +879,6 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
                           int accumulate, void* stream) {
   if (!shape_ok(s) || !dz || !wpacked_t || !dx) return YMS_ERR_INVALID;
   if (!view_ok(dz_ld, dz_off, s->cout) || !view_ok(dx_ld, dx_off, s->cin)) return YMS_ERR_INVALID;
-  PackGeo g = pack_geo(s, 1);
   NTParams p{};
   p.src = (const char*)dz;
   p.wp = (const char*)wpacked_t;
@@ -731,13 +886,36 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
   p.src_ld = dz_ld; p.src_off = dz_off; p.dst_ld = dx_ld; p.dst_off = dx_off;
   p.SH = s->ho; p.SW = s->wo; p.OW = s->w;
   p.stride = s->stride; p.pad = s->pad;
-  p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
-  p.M = s->n * s->h * s->w;
   p.Ncols = s->cin;
-  p.div_ow = make_fastdiv(s->w);
-  p.div_ohw = make_fastdiv(s->h * s->w);
+  p.OH = s->h; p.OWx = s->w;
   TileChoice tc = choose_tile(s->cin);
   hipStream_t st = (hipStream_t)stream;
+  if (s->stride == 2) {
+    Dg2Geo d = dg2_geo(s);
+    const int es = elem_size(s->dtype);
+    p.cpt = d.cpt;
+    p.M = 0;
+    for (int c = 0; c < 4; ++c) {
+      p.cls_M[c] = d.M[c];
+      p.cls_nkt[c] = d.nkt[c];
+      p.cls_Kc[c] = d.Kc[c];
+      p.cls_ntx[c] = d.ntx[c];
+      p.cls_c0y[c] = d.c0y[c];
+      p.cls_c0x[c] = d.c0x[c];
+      p.cls_woff[c] = d.off_elems[c] * es;
+      p.cls_div_w[c] = make_fastdiv(std::max(1, d.Wa[c]));
+      p.cls_div_hw[c] = make_fastdiv(std::max(1, d.Ha[c] * d.Wa[c]));
+      p.M = std::max(p.M, d.M[c]);
+    }
+    if (p.M == 0) return YMS_OK;
+    if (accumulate) return dispatch_nt<MODE_DGRAD2, EPI_ACCUM>(p, s->dtype, s->k, tc.cfg, st);
+    return dispatch_nt<MODE_DGRAD2, EPI_STORE>(p, s->dtype, s->k, tc.cfg, st);
+  }
+  PackGeo g = pack_geo(s, 1);
+  p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
+  p.M = s->n * s->h * s->w;
+  p.div_ow = make_fastdiv(s->w);
+  p.div_ohw = make_fastdiv(s->h * s->w);
   if (accumulate) return dispatch_nt<MODE_DGRAD, EPI_ACCUM>(p, s->dtype, s->k, tc.cfg, st);
   return dispatch_nt<MODE_DGRAD, EPI_STORE>(p, s->dtype, s->k, tc.cfg, st);
 }
@@ -777,8 +955,8 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
-  const long total = (long)s->cout * s->k * s->k * w.cin8;
-  dim3 g2((unsigned)std::min<long>(cdiv(total, 256), 8192));
+  const int kf = s->k * s->k * w.cin8;
+  dim3 g2((unsigned)(s->cout * cdiv(kf, 128)));
   hipLaunchKernelGGL(wgrad_reduce_kernel, g2, dim3(256), 0, st, ws, w.splits,
                      (long)w.slab_rows * w.slab_ld, w.slab_ld, s->cout, s->cin, w.cin8, s->k, dw, accumulate);
   return launch_status();

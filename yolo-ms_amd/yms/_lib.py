@@ -59,7 +59,7 @@ _SIGS = {
     "yms_bn_act_bwd_reduce": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
     "yms_bn_act_bwd_finalize": (_I, [_I, _P, _I, _L, _P, _P, _P, _P]),
     "yms_bn_act_bwd_apply": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _I, _P, _I, _I,
-                                  _P, _I, _I, _P]),
+                                  _P, _I, _I, _I, _P]),
     "yms_bias_bwd": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _P]),
     "yms_sppf_ws_bytes": (_SZ, [_I, _I, _I, _I]),
     "yms_sppf_pool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P]),
@@ -71,6 +71,7 @@ _SIGS = {
     "yms_nchw_to_nhwc": (_I, [_I, _I, _I, _I, _I, _I, _P, _P, _I, _I, _I, _P]),
     "yms_cast": (_I, [_I, _I, _L, _P, _P, _P]),
     "yms_zero": (_I, [_P, _SZ, _P]),
+    "yms_copy": (_I, [_P, _P, _SZ, _P]),
     "yms_head_decode": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P]),
     "yms_dfl": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "yms_nms_prep": (_I, [_I, _I, _I, _P, _F, _P, _P, _P, _P]),

@@ -86,6 +86,55 @@ class Layout:
         return off
 
 
+class GradTracker:
+    """Backward-order simulation deciding, for every write into an activation-gradient slice,
+    whether it is the first one (plain store) or must accumulate; buffers that are read
+    before any write (or carry zero-padded channels) are zeroed once per backward."""
+
+    def __init__(self):
+        self.written = {}
+        self.zero = set()
+
+    def _iv(self, v):
+        return v.off, v.off + v.c
+
+    def _covered(self, v):
+        lo, hi = self._iv(v)
+        ivs = sorted(self.written.get(v.buf.idx, []))
+        cur = lo
+        for a, b in ivs:
+            if a <= cur < b:
+                cur = b
+            if cur >= hi:
+                return True
+        return cur >= hi
+
+    def _touch(self, v):
+        lo, hi = self._iv(v)
+        return any(a < hi and lo < b for a, b in self.written.get(v.buf.idx, []))
+
+    def _zero_buf(self, v):
+        self.zero.add(v.buf.idx)
+        self.written[v.buf.idx] = [(0, v.buf.ld)]
+
+    def read(self, v):
+        if not self._covered(v):
+            self._zero_buf(v)
+
+    def write(self, v):
+        """-> accumulate flag (0 = first writer, plain store)."""
+        if v.buf.zero:                       # padded channels must stay zero: zero whole buffer
+            if v.buf.idx not in self.zero:
+                self._zero_buf(v)
+            return 1
+        if not self._touch(v):
+            self.written.setdefault(v.buf.idx, []).append(self._iv(v))
+            return 0
+        if not self._covered(v):
+            self._zero_buf(v)
+        return 1
+
+
 class Rt:
     """Per-call runtime state."""
 
@@ -184,6 +233,11 @@ class ConvOp:
         L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
                base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
 
+    def plan_grads(self, T):
+        T.read(self.y)
+        self.acc_res = T.write(self.res) if self.res is not None else 0
+        self.acc_x = T.write(self.x) if self.x.buf.needs_grad else 0
+
     def bwd(self, rt):
         x, y, r = self.x, self.y, self.res
         base, dt, c = rt.base, rt.plan.dt, self.c
@@ -198,9 +252,11 @@ class ConvOp:
         gres = rt.g(r) if r is not None else None
         gro = (r.buf.ld, r.off) if r is not None else (0, 0)
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
-               base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, gres, gro[0], gro[1], rt.st)
+               base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, gres, gro[0], gro[1], self.acc_res,
+               rt.st)
         if x.buf.needs_grad:
-            L.call("yms_conv_dgrad", self.sp, z, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off, 1, rt.st)
+            L.call("yms_conv_dgrad", self.sp, z, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                   self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             wsz = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
@@ -252,6 +308,10 @@ class BiasConvOp:
         L.call("yms_conv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, wp, rt.a(y), y.buf.ld, y.off,
                None, self.conv.bias.data_ptr(), L.ACT_NONE, None, 0, 0, None, rt.st)
 
+    def plan_grads(self, T):
+        T.read(self.y)
+        self.acc_x = T.write(self.x) if self.x.buf.needs_grad else 0
+
     def bwd(self, rt):
         x, y = self.x, self.y
         gy, gyl, gyo = rt.g(y), y.buf.ld, y.off
@@ -260,7 +320,8 @@ class BiasConvOp:
             L.call("yms_bias_bwd", rt.plan.dt, self.npix, self.c, gy, gyl, gyo,
                    rt.gbase + rt.plan.gscratch["bwd"], db, rt.st)
         if x.buf.needs_grad:
-            L.call("yms_conv_dgrad", self.sp, gy, gyl, gyo, rt.base + self.t_wpt, rt.g(x), x.buf.ld, x.off, 1, rt.st)
+            L.call("yms_conv_dgrad", self.sp, gy, gyl, gyo, rt.base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                   self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, gy, gyl, gyo,
@@ -285,10 +346,16 @@ class UpsampleOp:
         L.call("yms_upsample2x_fwd", rt.plan.dt, self.n, x.h, x.w, x.c, rt.a(x), x.buf.ld, x.off,
                rt.a(y), y.buf.ld, y.off, rt.st)
 
+    def plan_grads(self, T):
+        T.read(self.y)
+        self.acc_x = T.write(self.x) if self.x.buf.needs_grad else 0
+
     def bwd(self, rt):
         x, y = self.x, self.y
+        if not x.buf.needs_grad:
+            return
         L.call("yms_upsample2x_bwd", rt.plan.dt, self.n, x.h, x.w, x.c, rt.g(y), y.buf.ld, y.off,
-               rt.g(x), x.buf.ld, x.off, 1, rt.st)
+               rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
 
     def grad_params(self):
         return []
@@ -308,6 +375,9 @@ class SppfPoolOp:
     def fwd(self, rt):
         v = self.v
         L.call("yms_sppf_pool_fwd", rt.plan.dt, self.n, v.h, v.w, self.c, rt.a(v), v.buf.ld, v.off, rt.st)
+
+    def plan_grads(self, T):
+        T.read(self.v)        # slot grads come from conv2's dgrad; the pool chain accumulates in place
 
     def bwd(self, rt):
         v = self.v
@@ -395,6 +465,12 @@ class Plan:
         self.garena_bytes = Lg.size
         self.eval_bytes = Le.size
         self.zero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.zero]
+        if self.training:
+            T = GradTracker()
+            self.seed_acc = [T.write(v) for v in self.outputs]
+            for op in reversed(self.ops):
+                op.plan_grads(T)
+            self.gzero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.idx in T.zero]
         self.flops = sum(op.flops for op in self.ops)
         # parameter-gradient arena in backward-completion order (reverse op order)
         order = []

@@ -98,6 +98,22 @@ def _decode(plan, rt, arena):
     return out
 
 
+def _seed_grad(plan, rt, v, g, acc):
+    """Incoming output gradient -> NHWC grad slice.  Channels-last grads (what elementwise
+    losses on our channels-last outputs produce) are already NHWC: strided 2-D copy."""
+    n, c, h, w = g.shape
+    if (g.dtype == L_DTYPES[plan.dt] and g.stride(1) == 1 and g.stride(3) == c and g.stride(2) == w * c
+            and g.stride(0) == h * w * c and not acc and c == v.buf.ld and v.off == 0):
+        L.call("yms_copy", rt.g(v), g.data_ptr(), n * h * w * c * plan.es, rt.st)
+        return
+    gc = g.contiguous()
+    L.call("yms_nchw_to_nhwc", L.dtype_code(gc.dtype), plan.dt, n, h, w, c, gc.data_ptr(), rt.g(v), v.buf.ld,
+           v.off, acc, rt.st)
+
+
+L_DTYPES = {L.F32: torch.float32, L.BF16: torch.bfloat16, L.F16: torch.float16}
+
+
 class _PlanFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, state, *args):
@@ -129,13 +145,14 @@ class _PlanFn(torch.autograd.Function):
         rt.st = L.stream_ptr(dev)
         garena = torch.empty(max(plan.garena_bytes, 1), dtype=torch.uint8, device=dev)
         rt.gbase = garena.data_ptr()
-        L.call("yms_zero", rt.gbase, plan.act_bytes, rt.st)
-        for v, g in zip(plan.outputs, gouts):
+        for off, nb in plan.gzero_ranges:
+            L.call("yms_zero", rt.gbase + off, nb, rt.st)
+        for v, g, acc in zip(plan.outputs, gouts, plan.seed_acc):
             if g is None:
+                if not acc:
+                    L.call("yms_zero", rt.g(v), v.buf.npix * v.buf.ld * plan.es, rt.st)
                 continue
-            gc = g.contiguous()
-            L.call("yms_nchw_to_nhwc", L.dtype_code(gc.dtype), plan.dt, gc.shape[0], gc.shape[2], gc.shape[3],
-                   gc.shape[1], gc.data_ptr(), rt.g(v), v.buf.ld, v.off, 1, rt.st)
+            _seed_grad(plan, rt, v, g, acc)
         params = state.params
         need = [p.requires_grad for p in params]
         total = sum(params[i].numel() for i in plan.pgrad_order if need[i])
