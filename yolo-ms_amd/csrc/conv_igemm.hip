@@ -20,7 +20,8 @@
 
 namespace yms {
 
-constexpr int NT_ROWP = 80;  // bytes per LDS row (64 B of K + 16 B pad)
+constexpr int NT_KCH = 8;     // 16-B chunks of K per k-tile row (128 B)
+constexpr int NT_ROWP = 144;  // LDS pitch: 128 B + 16 B pad (conflict-free ds_read_b128 over 16 rows)
 
 enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD2 = 2 };  // DGRAD2: stride-2 dgrad by output parity
 enum { EPI_AFFINE = 0, EPI_STATS = 1, EPI_STORE = 2, EPI_ACCUM = 3 };
@@ -58,34 +59,32 @@ struct NTParams {
 
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16> {
-  static __device__ __forceinline__ f32x16 mma(const uint4& a, const uint4& b, f32x16 c) {
+  static __device__ __forceinline__ f32x16 mma(const u32x4& a, const u32x4& b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
                                                    __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
   }
 };
 template <> struct Mfma<f16> {
-  static __device__ __forceinline__ f32x16 mma(const uint4& a, const uint4& b, f32x16 c) {
+  static __device__ __forceinline__ f32x16 mma(const u32x4& a, const u32x4& b, f32x16 c) {
     return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
                                                   __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
   }
 };
 
-template <typename T>
-__device__ __forceinline__ void store_val(char* base, long idx, float v) {
-  reinterpret_cast<T*>(base)[idx] = (T)v;
-}
-
 template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN>
-__global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
+__global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int A_SLOTS = BM / 64;
-  constexpr int B_CHUNKS = BN * 4;
+  constexpr int RSTEP = 256 / NT_KCH;                      // rows covered by one load pass
+  constexpr int A_SLOTS = BM / RSTEP;
+  constexpr int B_CHUNKS = BN * NT_KCH;
   constexpr int B_SLOTS = (B_CHUNKS + 255) / 256;
   constexpr int TILE_BYTES = (BM + BN) * NT_ROWP;
+  constexpr int EPI_P = BN + 4;                            // fp32 staging pitch (floats)
+  constexpr int SMEM = (2 * TILE_BYTES > BM * EPI_P * 4) ? 2 * TILE_BYTES : BM * EPI_P * 4;
   constexpr bool F32 = sizeof(T) == 4;
-  static_assert(TM >= 1 && TN >= 1, "bad tile");
-  __shared__ __attribute__((aligned(16))) char smem[2 * TILE_BYTES];
+  static_assert(TM >= 1 && TN >= 1 && A_SLOTS >= 1, "bad tile");
+  __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -106,13 +105,13 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
     if (m0 >= M) return;   // uniform: this class has fewer row tiles
   }
 
-  // ---- im2col loader state (A side): fixed chunk column q, rows r0 + 64*i ----
-  const int q = tid & 3, r0 = tid >> 2;
+  // ---- im2col loader state (A side): fixed chunk column q, rows r0 + RSTEP*i ----
+  const int q = tid & (NT_KCH - 1), r0 = tid / NT_KCH;
   int a_base[A_SLOTS], a_y[A_SLOTS], a_x[A_SLOTS];
   bool a_ok[A_SLOTS];
 #pragma unroll
   for (int i = 0; i < A_SLOTS; ++i) {
-    const int m = m0 + r0 + 64 * i;
+    const int m = m0 + r0 + RSTEP * i;
     a_ok[i] = m < M;
     const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
     const uint32_t n = fdiv(mm, dv_hw);
@@ -133,10 +132,10 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
   }
   int tap = q / p.cpt, cc = q - (q / p.cpt) * p.cpt;
 
-  uint4 a_reg[A_SLOTS], b_reg[B_SLOTS];
+  u32x4 a_reg[A_SLOTS], b_reg[B_SLOTS];
 
   auto load_tile = [&](int kt) {
-    const int kc = kt * 4 + q;
+    const int kc = kt * NT_KCH + q;
     int kh, kw;
     if (MODE == MODE_DGRAD2) {
       kh = ntx == 1 ? tap : (tap >> 1);     // jy
@@ -170,22 +169,22 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
       ok = ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW;
       if (ok) {
         const long e = ((long)(a_base[i] + iy) * p.SW + ix) * p.src_ld + p.src_off;
-        a_reg[i] = *reinterpret_cast<const uint4*>(p.src + e * sizeof(T) + cc * 16);
+        a_reg[i] = *reinterpret_cast<const u32x4*>(p.src + e * sizeof(T) + cc * 16);
       } else {
-        a_reg[i] = make_uint4(0, 0, 0, 0);
+        a_reg[i] = u32x4{0u, 0u, 0u, 0u};
       }
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
       const int c = tid + 256 * j;
-      if (c < B_CHUNKS) {
-        const int row = c >> 2, qq = c & 3;
-        const long off = ((long)(n0 + row) * (nkt * 4) + kt * 4 + qq) * 16;
-        b_reg[j] = *reinterpret_cast<const uint4*>(wp + off);
+      if (B_CHUNKS >= 256 * (j + 1) || c < B_CHUNKS) {
+        const int row = c / NT_KCH, qq = c % NT_KCH;
+        const long off = ((long)(n0 + row) * (nkt * NT_KCH) + kt * NT_KCH + qq) * 16;
+        b_reg[j] = *reinterpret_cast<const u32x4*>(wp + off);
       }
     }
-    // advance the tap cursor by 4 chunks for the next k-tile
-    cc += 4;
+    // advance the tap cursor by one k-tile of chunks
+    cc += NT_KCH;
     while (cc >= p.cpt) { cc -= p.cpt; ++tap; }
   };
 
@@ -194,11 +193,12 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
     char* B = A + BM * NT_ROWP;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i)
-      *reinterpret_cast<uint4*>(A + (r0 + 64 * i) * NT_ROWP + q * 16) = a_reg[i];
+      *reinterpret_cast<u32x4*>(A + (r0 + RSTEP * i) * NT_ROWP + q * 16) = a_reg[i];
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
       const int c = tid + 256 * j;
-      if (c < B_CHUNKS) *reinterpret_cast<uint4*>(B + (c >> 2) * NT_ROWP + (c & 3) * 16) = b_reg[j];
+      if (B_CHUNKS >= 256 * (j + 1) || c < B_CHUNKS)
+        *reinterpret_cast<u32x4*>(B + (c / NT_KCH) * NT_ROWP + (c % NT_KCH) * 16) = b_reg[j];
     }
   };
 
@@ -211,52 +211,60 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.0f;
 
   const int lr = lane & 31, lh = lane >> 5;
-  auto compute = [&](int buf) {
+  // nch: valid 16-B chunks in this k-tile (the tail tile of K may be partial)
+  auto compute = [&](int buf, int nch) {
     const char* A = smem + buf * TILE_BYTES;
     const char* B = A + BM * NT_ROWP;
     if constexpr (!F32) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
-        uint4 af[TM], bfr[TN];
+      for (int s = 0; s < NT_KCH / 2; ++s) {
+        if (2 * s < nch) {
+          u32x4 af[TM], bfr[TN];
 #pragma unroll
-        for (int a = 0; a < TM; ++a)
-          af[a] = *reinterpret_cast<const uint4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
-#pragma unroll
-        for (int b = 0; b < TN; ++b)
-          bfr[b] = *reinterpret_cast<const uint4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[a], bfr[b], acc[a][b]);
-      }
-    } else {
-      // fp32: lane (r,h) holds k = 8h..8h+7 of its row; MFMA j pairs element j of both halves.
-      float af[TM][8], bfr[TN][8];
-#pragma unroll
-      for (int a = 0; a < TM; ++a) {
-        const float4* src = reinterpret_cast<const float4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 32 * lh);
-        float4 u = src[0], v = src[1];
-        af[a][0] = u.x; af[a][1] = u.y; af[a][2] = u.z; af[a][3] = u.w;
-        af[a][4] = v.x; af[a][5] = v.y; af[a][6] = v.z; af[a][7] = v.w;
-      }
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        const float4* src = reinterpret_cast<const float4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 32 * lh);
-        float4 u = src[0], v = src[1];
-        bfr[b][0] = u.x; bfr[b][1] = u.y; bfr[b][2] = u.z; bfr[b][3] = u.w;
-        bfr[b][4] = v.x; bfr[b][5] = v.y; bfr[b][6] = v.z; bfr[b][7] = v.w;
-      }
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
+          for (int a = 0; a < TM; ++a)
+            af[a] = *reinterpret_cast<const u32x4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
 #pragma unroll
           for (int b = 0; b < TN; ++b)
-            acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][j], bfr[b][j], acc[a][b], 0, 0, 0);
+            bfr[b] = *reinterpret_cast<const u32x4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
+#pragma unroll
+          for (int a = 0; a < TM; ++a)
+#pragma unroll
+            for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[a], bfr[b], acc[a][b]);
+        }
+      }
+    } else {
+      // fp32: per 64-B substep lane (r,h) holds k = 8h..8h+7; MFMA j pairs element j of both halves.
+#pragma unroll
+      for (int s = 0; s < NT_KCH / 4; ++s) {
+        if (4 * s < nch) {
+          float af[TM][8], bfr[TN][8];
+#pragma unroll
+          for (int a = 0; a < TM; ++a) {
+            const float4* src = reinterpret_cast<const float4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 64 * s + 32 * lh);
+            float4 u = src[0], v = src[1];
+            af[a][0] = u.x; af[a][1] = u.y; af[a][2] = u.z; af[a][3] = u.w;
+            af[a][4] = v.x; af[a][5] = v.y; af[a][6] = v.z; af[a][7] = v.w;
+          }
+#pragma unroll
+          for (int b = 0; b < TN; ++b) {
+            const float4* src = reinterpret_cast<const float4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 64 * s + 32 * lh);
+            float4 u = src[0], v = src[1];
+            bfr[b][0] = u.x; bfr[b][1] = u.y; bfr[b][2] = u.z; bfr[b][3] = u.w;
+            bfr[b][4] = v.x; bfr[b][5] = v.y; bfr[b][6] = v.z; bfr[b][7] = v.w;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j)
+#pragma unroll
+            for (int a = 0; a < TM; ++a)
+#pragma unroll
+              for (int b = 0; b < TN; ++b)
+                acc[a][b] = __builtin_amdgcn_mfma_f32_32x32x2f32(af[a][j], bfr[b][j], acc[a][b], 0, 0, 0);
+        }
+      }
     }
   };
 
-  // ---- main loop: register-staged double buffer, one barrier per k-tile ----
+  // ---- main loop: register-staged double buffer, one barrier per 128-B k-tile ----
   load_tile(0);
   store_tile(0);
   __syncthreads();
@@ -264,77 +272,105 @@ __global__ __launch_bounds__(256) void conv_nt_kernel(NTParams p) {
     const int cur = kt & 1;
     const bool more = kt + 1 < nkt;
     if (more) load_tile(kt + 1);
-    compute(cur);
+    compute(cur, Kc - kt * NT_KCH);
     if (more) store_tile(cur ^ 1);
     __syncthreads();
   }
 
-  // ---- epilogue ----
-  float s1[TN], s2[TN];
+  // ---- epilogue: stage the fp32 tile in LDS, then 16-B coalesced row segments ----
+  float* st = reinterpret_cast<float*>(smem);
 #pragma unroll
-  for (int b = 0; b < TN; ++b) { s1[b] = 0.f; s2[b] = 0.f; }
+  for (int a = 0; a < TM; ++a)
 #pragma unroll
-  for (int b = 0; b < TN; ++b) {
-    const int col = n0 + wn * WTN + b * 32 + lr;
-    const bool col_ok = col < p.Ncols;
-    float sc = 1.0f, sh = 0.0f;
-    if (EPI == EPI_AFFINE && col_ok) {
-      if (p.scale) sc = p.scale[col];
-      if (p.shift) sh = p.shift[col];
-    }
-#pragma unroll
-    for (int a = 0; a < TM; ++a) {
+    for (int b = 0; b < TN; ++b)
 #pragma unroll
       for (int i = 0; i < 16; ++i) {
-        int row = m0 + wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
-        float v = acc[a][b][i];
-        if (EPI == EPI_STATS) {
-          s1[b] += v;
-          s2[b] += v * v;
-        }
-        const bool row_ok = row < M;
-        if (MODE == MODE_DGRAD2 && row_ok) {
-          const uint32_t n = fdiv((uint32_t)row, dv_hw);
-          const uint32_t rem = (uint32_t)row - n * dv_hw.d;
-          const uint32_t ya = fdiv(rem, dv_w);
-          const uint32_t xb = rem - ya * dv_w.d;
-          row = ((int)n * p.OH + 2 * (int)ya + (cls >> 1)) * p.OWx + 2 * (int)xb + (cls & 1);
-        }
-        if (row_ok && col_ok) {
-          if (EPI == EPI_AFFINE) {
-            v = v * sc + sh;
-            if (p.act == YMS_ACT_SILU) v = silu_f(v);
-            if (p.res) v += (float)reinterpret_cast<const T*>(p.res)[(long)row * p.res_ld + p.res_off + col];
-          } else if (EPI == EPI_ACCUM) {
-            v += (float)reinterpret_cast<const T*>(p.dst)[(long)row * p.dst_ld + p.dst_off + col];
-          }
-          store_val<T>(p.dst, (long)row * p.dst_ld + p.dst_off + col, v);
-        }
+        const int rl = wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+        st[rl * EPI_P + wn * WTN + b * 32 + lr] = acc[a][b][i];
       }
+  __syncthreads();
+  constexpr int CH = BN / 8;              // 8-channel chunks per row
+  constexpr int RS = 256 / CH;            // row lanes
+  constexpr int NR = BM / RS;             // rows per thread
+  const int ch = tid % CH, rr = tid / CH;
+  const int col0 = n0 + ch * 8;
+  const int nv = p.Ncols - col0;          // valid channels in this chunk (may be <= 0)
+  float sc[8], sh[8], s1[8], s2[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    sc[i] = 1.0f;
+    sh[i] = 0.0f;
+    s1[i] = 0.0f;
+    s2[i] = 0.0f;
+    if (EPI == EPI_AFFINE && i < nv) {
+      if (p.scale) sc[i] = p.scale[col0 + i];
+      if (p.shift) sh[i] = p.shift[col0 + i];
     }
   }
-  if (EPI == EPI_STATS) {
-    float* red = reinterpret_cast<float*>(smem);  // [WGM][2][BN]
 #pragma unroll
-    for (int b = 0; b < TN; ++b) {
-      float t1 = s1[b] + __shfl_xor(s1[b], 32);
-      float t2 = s2[b] + __shfl_xor(s2[b], 32);
-      if (lh == 0) {
-        red[(wm * 2 + 0) * BN + wn * WTN + b * 32 + lr] = t1;
-        red[(wm * 2 + 1) * BN + wn * WTN + b * 32 + lr] = t2;
+  for (int j = 0; j < NR; ++j) {
+    const int rl = rr + RS * j;
+    int row = m0 + rl;
+    float v[8];
+    const float4 u0 = *reinterpret_cast<const float4*>(st + rl * EPI_P + ch * 8);
+    const float4 u1 = *reinterpret_cast<const float4*>(st + rl * EPI_P + ch * 8 + 4);
+    v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
+    v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
+    if (EPI == EPI_STATS) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        s1[i] += v[i];
+        s2[i] += v[i] * v[i];
       }
+    }
+    if (row >= M || nv <= 0) continue;
+    if (MODE == MODE_DGRAD2) {
+      const uint32_t n = fdiv((uint32_t)row, dv_hw);
+      const uint32_t rem = (uint32_t)row - n * dv_hw.d;
+      const uint32_t ya = fdiv(rem, dv_w);
+      const uint32_t xb = rem - ya * dv_w.d;
+      row = ((int)n * p.OH + 2 * (int)ya + (cls >> 1)) * p.OWx + 2 * (int)xb + (cls & 1);
+    }
+    T* dst = reinterpret_cast<T*>(p.dst) + (long)row * p.dst_ld + p.dst_off + col0;
+    if (EPI == EPI_AFFINE) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float a = v[i] * sc[i] + sh[i];
+        if (p.act == YMS_ACT_SILU) a = silu_f(a);
+        v[i] = a;
+      }
+      if (p.res) {
+        float r[8];
+        load8(reinterpret_cast<const T*>(p.res) + (long)row * p.res_ld + p.res_off + col0, nv, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += r[i];
+      }
+    } else if (EPI == EPI_ACCUM) {
+      float r[8];
+      load8(dst, nv, r);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) v[i] += r[i];
+    }
+    store8(dst, nv, v);
+  }
+  if (EPI == EPI_STATS) {
+    __syncthreads();                      // staging tile no longer read
+    float* red = reinterpret_cast<float*>(smem);  // [2][RS][BN]
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      red[rr * BN + ch * 8 + i] = s1[i];
+      red[RS * BN + rr * BN + ch * 8 + i] = s2[i];
     }
     __syncthreads();
     if (tid < BN) {
       float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-      for (int w = 0; w < WGM; ++w) {
-        t1 += red[(w * 2 + 0) * BN + tid];
-        t2 += red[(w * 2 + 1) * BN + tid];
+      for (int w = 0; w < RS; ++w) {
+        t1 += red[w * BN + tid];
+        t2 += red[RS * BN + w * BN + tid];
       }
-      float* st = p.stats + (long)tile_m * 2 * p.stats_ld;
-      st[n0 + tid] = t1;
-      st[p.stats_ld + n0 + tid] = t2;
+      float* so = p.stats + (long)tile_m * 2 * p.stats_ld;
+      so[n0 + tid] = t1;
+      so[p.stats_ld + n0 + tid] = t2;
     }
   }
 }
@@ -396,7 +432,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
     b_kh[j] = t / KS;
     b_kw[j] = t - b_kh[j] * KS;
   }
-  uint4 a_reg[A_SLOTS], b_reg[B_SLOTS];
+  u32x4 a_reg[A_SLOTS], b_reg[B_SLOTS];
 
   auto load_tile = [&](int kt) {
     const int q0 = kt * 32;
@@ -407,9 +443,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
       const int qpix = q0 + row;
       const int ch = m0 + col * EPC;
       if (c < 32 * CA && qpix < p.M && ch < p.cout8)
-        a_reg[i] = *reinterpret_cast<const uint4*>(p.dz + ((long)qpix * p.dz_ld + p.dz_off + ch) * SZ);
+        a_reg[i] = *reinterpret_cast<const u32x4*>(p.dz + ((long)qpix * p.dz_ld + p.dz_off + ch) * SZ);
       else
-        a_reg[i] = make_uint4(0, 0, 0, 0);
+        a_reg[i] = u32x4{0u, 0u, 0u, 0u};
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
@@ -425,9 +461,9 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
       ok = ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW;
       if (ok) {
         const long e = (((long)n * p.SH + iy) * p.SW + ix) * p.x_ld + p.x_off;
-        b_reg[j] = *reinterpret_cast<const uint4*>(p.x + e * SZ + b_cc[j] * 16);
+        b_reg[j] = *reinterpret_cast<const u32x4*>(p.x + e * SZ + b_cc[j] * 16);
       } else {
-        b_reg[j] = make_uint4(0, 0, 0, 0);
+        b_reg[j] = u32x4{0u, 0u, 0u, 0u};
       }
     }
   };
@@ -437,12 +473,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
       const int c = tid + 256 * i;
-      if (c < 32 * CA) *reinterpret_cast<uint4*>(A + (c / CA) * PA + (c % CA) * 16) = a_reg[i];
+      if (c < 32 * CA) *reinterpret_cast<u32x4*>(A + (c / CA) * PA + (c % CA) * 16) = a_reg[i];
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
       const int c = tid + 256 * j;
-      if (c < 32 * CB) *reinterpret_cast<uint4*>(B + b_row[j] * PB + b_col[j] * 16) = b_reg[j];
+      if (c < 32 * CB) *reinterpret_cast<u32x4*>(B + b_row[j] * PB + b_col[j] * 16) = b_reg[j];
     }
   };
 
@@ -465,7 +501,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
     if constexpr (!F32) {
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
-        uint4 af[TM], bfr[TN];
+        u32x4 af[TM], bfr[TN];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
           const int col = wm * WTM + a * 32 + tcb + 4 * pp;
@@ -475,7 +511,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
           s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p0);
           s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p1);
           uint2 u0 = __builtin_bit_cast(uint2, v0), u1 = __builtin_bit_cast(uint2, v1);
-          af[a] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+          af[a] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
 #pragma unroll
         for (int b = 0; b < TN; ++b) {
@@ -486,7 +522,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
           s16x4 v0 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p0);
           s16x4 v1 = __builtin_amdgcn_ds_read_tr16_b64_v4i16((YMS_LDS s16x4*)p1);
           uint2 u0 = __builtin_bit_cast(uint2, v0), u1 = __builtin_bit_cast(uint2, v1);
-          bfr[b] = make_uint4(u0.x, u0.y, u1.x, u1.y);
+          bfr[b] = u32x4{u0.x, u0.y, u1.x, u1.y};
         }
 #pragma unroll
         for (int a = 0; a < TM; ++a)
@@ -652,8 +688,8 @@ static PackGeo pack_geo(const yms_conv_shape* s, int for_dgrad) {
   g.c8_in = (int)rup(cin_k, 8);
   g.cpt = g.c8_in * es / 16;
   g.kc = s->k * s->k * g.cpt;
-  g.nkt = cdiv(g.kc, 4);
-  g.kp_elems = g.nkt * 64 / es;
+  g.nkt = cdiv(g.kc, NT_KCH);
+  g.kp_elems = g.nkt * NT_KCH * 16 / es;
   g.rows = (int)rup(cout_r, 128);
   return g;
 }
@@ -683,8 +719,8 @@ static Dg2Geo dg2_geo(const yms_conv_shape* s) {
     g.Wa[c] = (s->w - rx + 1) / 2;
     g.M[c] = s->n * g.Ha[c] * g.Wa[c];
     g.Kc[c] = g.nty[c] * g.ntx[c] * g.cpt;
-    g.nkt[c] = std::max(1, cdiv(g.Kc[c], 4));
-    g.kp[c] = g.nkt[c] * 64 / es;
+    g.nkt[c] = std::max(1, cdiv(g.Kc[c], NT_KCH));
+    g.kp[c] = g.nkt[c] * NT_KCH * 16 / es;
     g.off_elems[c + 1] = g.off_elems[c] + (long)g.rows * g.kp[c];
   }
   return g;
@@ -724,12 +760,12 @@ static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
     hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 128, 2, 2>), grid, dim3(256), 0, st, p);
   } else if (cfg == 1) {
     p.tiles_n = cdiv(p.Ncols, 64);
-    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n), gy);
-    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 256, 64, 4, 1>), grid, dim3(256), 0, st, p);
+    dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 64, 2, 2>), grid, dim3(256), 0, st, p);
   } else {
     p.tiles_n = cdiv(p.Ncols, 32);
-    dim3 grid((unsigned)(cdiv(p.M, 256) * p.tiles_n), gy);
-    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 256, 32, 4, 1>), grid, dim3(256), 0, st, p);
+    dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 32, 4, 1>), grid, dim3(256), 0, st, p);
   }
 }
 
@@ -746,7 +782,7 @@ static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hip
   return launch_status();
 }
 
-static int rows_for(int M, int cfg) { return cdiv(M, cfg == 0 ? 128 : 256); }
+static int rows_for(int M, int cfg) { (void)cfg; return cdiv(M, 128); }
 
 struct WgradPlan {
   int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc;

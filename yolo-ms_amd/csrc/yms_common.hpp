@@ -18,6 +18,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // 16-B register chunk (SROA-friendly, unlike HIP's uint4 struct)
 
 #define YMS_LDS __attribute__((address_space(3)))
 
