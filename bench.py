@@ -186,12 +186,17 @@ def main():
 
     # ---------------- inference (configs[1]) ----------------
     if rank == 0 and a.mode in ("both", "infer") and not a.no_infer:
-        model.eval()
+        # a fresh random-init model (SURVEY 8d input set 1: ~8400 candidates/image, ~105/class);
+        # the surrogate-trained weights above collapse every logit to ~0 (all classes tie).
+        torch.manual_seed(0)
+        imodel = YOLOv8(a.version, a.nc).to(dev).eval()
+        imodel.head.stride = torch.tensor([8.0, 16.0, 32.0])
+        set_compute_dtype(imodel, dtype)
         xi = torch.randn(a.infer_batch, 3, a.size, a.size, device=dev,
                          generator=torch.Generator(device=dev).manual_seed(99))
 
         def infer_step():
-            y = model(xi)
+            y = imodel(xi)
             yops.batched_nms_indices(y, 0.25, 0.45)
 
         dti = timed(infer_step, a.steps, a.warmup, 1)

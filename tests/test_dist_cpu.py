@@ -1,0 +1,107 @@
+"""CPU tier: the data-parallel layer (yms.dist) over gloo with world_size 2.
+
+The GPU path issues the same calls over RCCL ("nccl" backend, ReduceOp.AVG); here gloo
+(SUM + divide) exercises bucketing, completion-order triggering, averaging, parameter
+broadcast and BN-buffer broadcast without a GPU."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+
+class _Op:
+    def __init__(self, params):
+        self.params = params
+
+    def grad_params(self):
+        return self.params
+
+
+class _Plan:
+    """Mimics yms.plan.Plan: ops in forward order, params owned by ops."""
+
+    def __init__(self, sizes):
+        self.ops = [_Op([2 * i, 2 * i + 1]) for i in range(len(sizes) // 2)]
+        order = []
+        for op in reversed(self.ops):
+            order += op.grad_params()
+        self.pgrad_order = order
+        self.sizes = sizes
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from yms.dist import DataParallel, GradBucketer
+        sizes = [1000, 10, 5000, 20, 300, 3, 70000, 64]
+        plan = _Plan(sizes)
+        views = [None] * len(sizes)
+        total = sum(sizes)
+        pg = torch.empty(total)
+        off = 0
+        for i in plan.pgrad_order:
+            views[i] = pg[off:off + sizes[i]]
+            off += sizes[i]
+        bk = GradBucketer(bucket_cap_mb=0.02)      # ~5K floats per bucket -> several buckets
+        launched = []
+        for it in range(2):                          # twice: cached bucket layout
+            for i in plan.pgrad_order:
+                views[i].copy_(torch.arange(sizes[i], dtype=torch.float32) * (rank + 1) + i)
+            bk.begin(plan, pg, None, views)
+            for op in reversed(plan.ops):
+                # a bucket must only be launched once all its params are written
+                bk.op_done(op)
+            launched.append(bk.launched_buckets)
+            bk.finish()
+        exp = []
+        for i in plan.pgrad_order:
+            base = torch.arange(sizes[i], dtype=torch.float32)
+            exp.append(base * (1 + world) / 2 + i)   # mean over ranks of base*(r+1)+i
+        ok_grad = torch.allclose(pg, torch.cat(exp))
+        # parameter + BN buffer broadcast from rank 0
+        torch.manual_seed(rank)
+        m = torch.nn.BatchNorm2d(4)
+        with torch.no_grad():
+            m.weight.fill_(rank + 1.0)
+            m.running_mean.fill_(10.0 * (rank + 1))
+        dp = DataParallel(m, bucket_cap_mb=1.0)
+        ok_bcast = bool(torch.all(m.weight == 1.0)) and bool(torch.all(m.running_mean == 10.0))
+        with torch.no_grad():
+            m.running_mean.fill_(5.0 * (rank + 1))
+        dp.train()
+        dp(torch.zeros(2, 4, 3, 3))                   # buffers re-synced before forward
+        q.put((rank, ok_grad, launched, ok_bcast, m.running_mean[0].item()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_bucketed_allreduce_gloo_world2():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=120) for _ in range(world)]
+    for p in procs:
+        p.join(timeout=60)
+    for rank, ok_grad, launched, ok_bcast, rm in res:
+        assert ok_grad, rank
+        assert launched[0] == launched[1] >= 3, launched
+        assert ok_bcast, rank
+        # rank 0's buffer (5.0) broadcast before forward, then BN2d(momentum 0.1) on zeros
+        assert abs(rm - 0.9 * 5.0) < 1e-5, rm

@@ -739,15 +739,15 @@ static bool view_ok(int ld, int off, int c) { return ld % 8 == 0 && off % 8 == 0
 
 struct TileChoice { int cfg, bn; };
 static TileChoice choose_tile(int ncols) {
-  // minimise padded columns; prefer wider tiles on ties
-  const int bns[3] = {128, 64, 32};
-  int best = 0;
-  long bestpad = 1l << 40;
-  for (int i = 0; i < 3; ++i) {
-    long pad = rup(ncols, bns[i]);
-    if (pad < bestpad) { bestpad = pad; best = i; }
-  }
-  return TileChoice{best, bns[best]};
+  // One column tile whenever N <= 128: every extra column tile re-reads the whole im2col
+  // A operand, which costs more than the padded MFMA columns at these sizes.
+  if (ncols <= 32) return TileChoice{2, 32};
+  if (ncols <= 64) return TileChoice{1, 64};
+  if (ncols <= 128) return TileChoice{0, 128};
+  // wider: 128-column tiles unless that pads by more than 25%
+  const long p128 = rup(ncols, 128), p64 = rup(ncols, 64);
+  if (p128 * 4 > ncols * 5 && p64 < p128) return TileChoice{1, 64};
+  return TileChoice{0, 128};
 }
 
 template <typename T, int KS, int MODE, int EPI>

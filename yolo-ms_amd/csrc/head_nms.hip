@@ -32,10 +32,15 @@ struct DecodeParams {
   int* label;
 };
 
+// 16 lanes per anchor: lanes 0..3 each own one DFL side (16 contiguous bins), all 16 lanes
+// stride over the classes, so the 64+nc logits of an anchor are read and its 4+nc outputs
+// written as contiguous lane-consecutive segments (NHWC makes an anchor's logits contiguous).
 template <typename T>
-__global__ void head_decode_kernel(DecodeParams p) {
+__global__ __launch_bounds__(256) void head_decode_kernel(DecodeParams p) {
+  const int sub = threadIdx.x & 15;
   const long total = (long)p.n * p.A;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * (blockDim.x >> 4);
+  for (long t = blockIdx.x * (long)(blockDim.x >> 4) + (threadIdx.x >> 4); t < total; t += stride) {
     const int b = (int)(t / p.A);
     const int a = (int)(t - (long)b * p.A);
     int l = 0;
@@ -43,15 +48,13 @@ __global__ void head_decode_kernel(DecodeParams p) {
     const int r = a - p.aoff[l];
     const int y = r / p.w[l], x = r - (r / p.w[l]) * p.w[l];
     const T* src = reinterpret_cast<const T*>(p.lvl[l]) + (((long)b * p.h[l] + y) * p.w[l] + x) * p.no_ld;
-    float d[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float v[16];
-      float vv[8];
-      Vec8<T>::load(src + 16 * k, vv);
+    float dist = 0.f;
+    if (sub < 4) {
+      float v[16], vv[8];
+      Vec8<T>::load(src + 16 * sub, vv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[i] = vv[i];
-      Vec8<T>::load(src + 16 * k + 8, vv);
+      Vec8<T>::load(src + 16 * sub + 8, vv);
 #pragma unroll
       for (int i = 0; i < 8; ++i) v[8 + i] = vv[i];
       float m = v[0];
@@ -64,50 +67,76 @@ __global__ void head_decode_kernel(DecodeParams p) {
         s += ex;
         e += ex * (float)i;
       }
-      d[k] = e / s;
+      dist = e / s;
     }
+    // gather the 4 distances (lanes 0..3 of this 16-lane group)
+    const int base = (threadIdx.x & 63) & ~15;
+    const float d0 = __shfl(dist, base + 0), d1 = __shfl(dist, base + 1);
+    const float d2 = __shfl(dist, base + 2), d3 = __shfl(dist, base + 3);
     const float ax = (float)x + 0.5f, ay = (float)y + 0.5f, st = p.stride[l];
-    const float a0 = ax - d[0], a1 = ay - d[1];
-    const float b0 = ax + d[2], b1 = ay + d[3];
+    const float a0 = ax - d0, a1 = ay - d1;
+    const float b0 = ax + d2, b1 = ay + d3;
     const float cx = ((a0 + b0) / 2) * st, cy = ((a1 + b1) / 2) * st;
     const float bw = (b0 - a0) * st, bh = (b1 - a1) * st;
     float* o = p.out + t * (4 + p.nc);
-    o[0] = cx; o[1] = cy; o[2] = bw; o[3] = bh;
-    float best = 0.f;
-    int bl = 0;
+    if (sub == 0) { o[0] = cx; o[1] = cy; o[2] = bw; o[3] = bh; }
+    // classes: lane `sub` handles c = sub + 16k; best = (max prob, first index)
+    float best = -1.0f;
+    int bl = 0x7fffffff;
     const T* cls = src + 64;
-    for (int c = 0; c < p.nc; ++c) {
+    for (int c = sub; c < p.nc; c += 16) {
       const float pr = 1.0f / (1.0f + expf(-(float)cls[c]));
       o[4 + c] = pr;
-      if (c == 0 || pr > best) { best = pr; bl = c; }
+      if (pr > best) { best = pr; bl = c; }
     }
     if (p.score) {
-      p.bxy[t * 4 + 0] = cx - bw / 2;
-      p.bxy[t * 4 + 1] = cy - bh / 2;
-      p.bxy[t * 4 + 2] = cx + bw / 2;
-      p.bxy[t * 4 + 3] = cy + bh / 2;
-      p.score[t] = best;
-      p.label[t] = best > p.conf ? bl : -1;
+#pragma unroll
+      for (int off = 8; off > 0; off >>= 1) {
+        const float ob = __shfl_xor(best, off, 16);
+        const int ol = __shfl_xor(bl, off, 16);
+        if (ob > best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+      }
+      if (sub == 0) {
+        p.bxy[t * 4 + 0] = cx - bw / 2;
+        p.bxy[t * 4 + 1] = cy - bh / 2;
+        p.bxy[t * 4 + 2] = cx + bw / 2;
+        p.bxy[t * 4 + 3] = cy + bh / 2;
+        p.score[t] = best;
+        p.label[t] = best > p.conf ? bl : -1;
+      }
     }
   }
 }
 
-__global__ void nms_prep_kernel(int n, int A, int nc, const float* pred, float conf, float* bxy,
-                                float* score, int* label) {
+__global__ __launch_bounds__(256) void nms_prep_kernel(int n, int A, int nc, const float* pred, float conf,
+                                                       float* bxy, float* score, int* label) {
+  const int sub = threadIdx.x & 15;
   const long total = (long)n * A;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const long stride = (long)gridDim.x * (blockDim.x >> 4);
+  for (long t = blockIdx.x * (long)(blockDim.x >> 4) + (threadIdx.x >> 4); t < total; t += stride) {
     const float* q = pred + t * (4 + nc);
-    const float cx = q[0], cy = q[1], w = q[2], h = q[3];
-    bxy[t * 4 + 0] = cx - w / 2;
-    bxy[t * 4 + 1] = cy - h / 2;
-    bxy[t * 4 + 2] = cx + w / 2;
-    bxy[t * 4 + 3] = cy + h / 2;
-    float best = q[4];
-    int bl = 0;
-    for (int c = 1; c < nc; ++c)
-      if (q[4 + c] > best) { best = q[4 + c]; bl = c; }
-    score[t] = best;
-    label[t] = best > conf ? bl : -1;
+    float best = -INFINITY;
+    int bl = 0x7fffffff;
+    bool any = false;
+    for (int c = sub; c < nc; c += 16) {
+      const float v = q[4 + c];
+      if (!any || v > best) { best = v; bl = c; any = true; }
+    }
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) {
+      const float ob = __shfl_xor(best, off, 16);
+      const int ol = __shfl_xor(bl, off, 16);
+      if (ob > best || (ob == best && ol < bl)) { best = ob; bl = ol; }
+    }
+    if (sub == 0) {
+      const float cx = q[0], cy = q[1], w = q[2], h = q[3];
+      bxy[t * 4 + 0] = cx - w / 2;
+      bxy[t * 4 + 1] = cy - h / 2;
+      bxy[t * 4 + 2] = cx + w / 2;
+      bxy[t * 4 + 3] = cy + h / 2;
+      score[t] = best;
+      label[t] = best > conf ? bl : -1;
+    }
   }
 }
 
@@ -141,73 +170,72 @@ struct NmsWs {
   int* scratch;      // [n][A]
   int* cls_cnt;      // [n][nc]
   int* cls_off;      // [n][nc]
+  int* big;          // [0] = count, then (b, c) pairs of segments with more than NMS_CAP boxes
+  uint64_t* mask;    // [n][A][ceil(A/64)] suppression bitmask rows of the big segments
+  int words;         // ceil(A/64)
 };
 
-__global__ __launch_bounds__(256) void nms_class_kernel(int A, int nc, const float* bxy,
-                                                        const float* score, const int* label,
-                                                        double thr, NmsWs ws) {
+// Per image: class histogram, exclusive scan and scatter of (score, anchor) keys into class
+// buckets of ws.gkeys[b][A] (bucket order is irrelevant: the key is a total order).
+__global__ __launch_bounds__(1024) void nms_bucket_kernel(int A, int nc, const float* score, const int* label,
+                                                          NmsWs ws) {
+  extern __shared__ int s_cnt[];      // [nc] counts, then [nc] cursors
+  int* s_cur = s_cnt + nc;
+  const int b = blockIdx.x;
+  const int* lab = label ? label + (long)b * A : nullptr;
+  const float* sc = score + (long)b * A;
+  for (int c = threadIdx.x; c < 2 * nc; c += blockDim.x) s_cnt[c] = 0;
+  __syncthreads();
+  for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    const int l = lab ? lab[a] : 0;
+    if (l >= 0) atomicAdd(&s_cnt[l], 1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int run = 0;
+    for (int c = 0; c < nc; ++c) {
+      const int k = s_cnt[c];
+      s_cur[c] = run;
+      ws.cls_off[(long)b * nc + c] = run;
+      ws.cls_cnt[(long)b * nc + c] = k;    // candidates (rewritten with kept count by the NMS pass)
+      if (k > NMS_CAP) {
+        const int slot = atomicAdd(ws.big, 1);
+        ws.big[1 + 2 * slot] = b;
+        ws.big[2 + 2 * slot] = c;
+      }
+      run += k;
+    }
+  }
+  __syncthreads();
+  uint64_t* keys = ws.gkeys + (long)b * A;
+  for (int a = threadIdx.x; a < A; a += blockDim.x) {
+    const int l = lab ? lab[a] : 0;
+    if (l < 0) continue;
+    const int pos = atomicAdd(&s_cur[l], 1);
+    keys[pos] = ((uint64_t)(~orderable(sc[a])) << 32) | (uint32_t)a;
+  }
+}
+
+__global__ __launch_bounds__(256) void nms_class_kernel(int A, int nc, const float* bxy, double thr, NmsWs ws) {
   __shared__ uint64_t s_keys[NMS_CAP];
   __shared__ float4 s_boxes[NMS_CAP];
-  __shared__ int s_red[2][4];
   __shared__ int s_nkept;
   __shared__ unsigned long long s_sup[4];
 
   const int c = blockIdx.x, b = blockIdx.y;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int* lab = label ? label + (long)b * A : nullptr;
-
-  // pass 1: count (label < c) and (label == c)
-  int lt = 0, eq = 0;
-  for (int a = tid; a < A; a += 256) {
-    const int l = lab ? lab[a] : 0;
-    lt += (l >= 0 && l < c);
-    eq += (l == c);
-  }
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    lt += __shfl_xor(lt, o);
-    eq += __shfl_xor(eq, o);
-  }
-  if (lane == 0) { s_red[0][wave] = lt; s_red[1][wave] = eq; }
-  __syncthreads();
-  const int off = s_red[0][0] + s_red[0][1] + s_red[0][2] + s_red[0][3];
-  const int n = s_red[1][0] + s_red[1][1] + s_red[1][2] + s_red[1][3];
-  if (tid == 0) {
-    ws.cls_off[(long)b * nc + c] = off;
-    ws.cls_cnt[(long)b * nc + c] = 0;
-  }
-  if (n == 0) return;
-  const bool big = n > NMS_CAP;
-  uint64_t* keys = big ? ws.gkeys + (long)b * A + off : s_keys;
+  const int n = ws.cls_cnt[(long)b * nc + c];
+  if (n == 0 || n > NMS_CAP) return;      // big segments: nms_big_kernel
+  const int off = ws.cls_off[(long)b * nc + c];
+  const bool big = false;
+  uint64_t* gk = ws.gkeys + (long)b * A + off;
+  uint64_t* keys = big ? gk : s_keys;
   float4* boxes = big ? ws.gboxes + (long)b * A + off : s_boxes;
   int* out = ws.scratch + (long)b * A + off;
   const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
-  const float* sc = score + (long)b * A;
+  if (!big)
+    for (int i = tid; i < n; i += 256) s_keys[i] = gk[i];
   __syncthreads();
-
-  // pass 2: stable ordered compaction of this class' anchors into keys
-  int base = 0;
-  for (int a0 = 0; a0 < A; a0 += 256) {
-    const int a = a0 + tid;
-    const bool f = a < A && (lab ? lab[a] == c : true);
-    const unsigned long long m = __ballot(f);
-    const int pre = __popcll(m & ((1ull << lane) - 1ull));
-    if (lane == 0) s_red[0][wave] = __popcll(m);
-    __syncthreads();
-    int wpre = 0, tot = 0;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const int cnt = s_red[0][w];
-      wpre += (w < wave) ? cnt : 0;
-      tot += cnt;
-    }
-    if (f) {
-      const uint32_t okey = ~orderable(sc[a]);
-      keys[base + wpre + pre] = ((uint64_t)okey << 32) | (uint32_t)a;
-    }
-    base += tot;
-    __syncthreads();
-  }
 
   // bitonic sort (direction-free flip formulation; virtual +inf padding beyond n)
   int N2 = 1;
@@ -270,6 +298,166 @@ __global__ __launch_bounds__(256) void nms_class_kernel(int A, int nc, const flo
   if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nkept;
 }
 
+// Large segments (> NMS_CAP boxes: nc=1, or one dominant class of a random-init model).
+//  nms_big_sort : one 1024-thread block per segment, bitonic sort (LDS when <= 16K keys),
+//                 sorted boxes + anchor ids to global.
+//  nms_big_mask : GPU-wide; one wave per (segment, 64-row block), lane = row, 64-bit words of
+//                 "IoU(i, j) > thr, j > i".  Disjoint boxes take an early exit (ovr = 0, or
+//                 0/0 = NaN, is never > thr for thr >= 0), the ratio compare uses the float
+//                 threshold exactly equivalent to torchvision's double compare.
+//  nms_big_scan : blocked greedy: for 64-candidate block k all 1024 threads OR word k of the
+//                 rows kept so far, then one wave resolves the block's own 64x64 diagonal.
+constexpr int NMS_BIG_LDS_KEYS = 16384;
+
+__device__ __forceinline__ bool iou_gt_f(const float4& i, const float4& j, float thr_f, bool full) {
+  const float xx1 = fmaxf(i.x, j.x);
+  const float yy1 = fmaxf(i.y, j.y);
+  const float xx2 = fminf(i.z, j.z);
+  const float yy2 = fminf(i.w, j.w);
+  if (!full && (xx2 <= xx1 || yy2 <= yy1)) return false;   // inter == 0
+  const float iarea = (i.z - i.x) * (i.w - i.y);
+  const float jarea = (j.z - j.x) * (j.w - j.y);
+  const float w = fmaxf(0.0f, xx2 - xx1);
+  const float h = fmaxf(0.0f, yy2 - yy1);
+  const float inter = w * h;
+  const float ovr = inter / (iarea + jarea - inter);
+  return ovr > thr_f;
+}
+
+__global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const float* bxy, NmsWs ws) {
+  extern __shared__ uint64_t s_big[];
+  const int tid = threadIdx.x;
+  const int nbig = ws.big[0];
+  for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
+    const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
+    const int n = ws.cls_cnt[(long)b * nc + c];
+    const int off = ws.cls_off[(long)b * nc + c];
+    uint64_t* gk = ws.gkeys + (long)b * A + off;
+    const bool inlds = n <= NMS_BIG_LDS_KEYS;
+    uint64_t* keys = inlds ? s_big : gk;
+    if (inlds)
+      for (int i = tid; i < n; i += 1024) s_big[i] = gk[i];
+    __syncthreads();
+    int N2 = 1;
+    while (N2 < n) N2 <<= 1;
+    for (int k = 2; k <= N2; k <<= 1) {
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int t = tid; t < N2; t += 1024) {
+          const int partner = (j == (k >> 1)) ? (t ^ (k - 1)) : (t ^ j);
+          if (partner > t && partner < n) {
+            const uint64_t x = keys[t], y = keys[partner];
+            if (y < x) { keys[t] = y; keys[partner] = x; }
+          }
+        }
+        __syncthreads();
+      }
+    }
+    float4* boxes = ws.gboxes + (long)b * A + off;
+    const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
+    int* idx = ws.scratch + (long)b * A + off;
+    for (int i = tid; i < n; i += 1024) {
+      const uint32_t a = (uint32_t)keys[i];
+      boxes[i] = bx[a];
+      idx[i] = (int)a;
+    }
+    __syncthreads();
+  }
+}
+
+__global__ __launch_bounds__(256) void nms_big_mask_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
+  // 4 waves: rows rb*64 .. +63 (one per lane), words w = rb + wave, rb + wave + 4, ...; the 64
+  // column boxes (and their areas) of a word are staged once in LDS and read as broadcasts.
+  __shared__ float4 s_box[4][64];
+  __shared__ float s_area[4][64];
+  const int nbig = ws.big[0];
+  const int rb = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  for (int it = blockIdx.y; it < nbig; it += gridDim.y) {
+    const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
+    const int n = ws.cls_cnt[(long)b * nc + c];
+    if (rb * 64 >= n) continue;
+    const int off = ws.cls_off[(long)b * nc + c];
+    const float4* boxes = ws.gboxes + (long)b * A + off;
+    uint64_t* mrow = ws.mask + ((long)b * A + off) * ws.words;
+    const int i = rb * 64 + lane;
+    const int W = (n + 63) >> 6;
+    const float4 bi = i < n ? boxes[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+    const float iarea = (bi.z - bi.x) * (bi.w - bi.y);
+    for (int w = rb + wave; w < W; w += 4) {
+      const int jl = (w << 6) + lane;
+      const float4 bj = jl < n ? boxes[jl] : make_float4(0.f, 0.f, 0.f, 0.f);
+      s_box[wave][lane] = bj;
+      s_area[wave][lane] = (bj.z - bj.x) * (bj.w - bj.y);
+      __builtin_amdgcn_wave_barrier();
+      uint64_t bits = 0;
+      const int jmax = min(64, n - (w << 6));
+      const int jmin = (w == rb) ? lane + 1 : 0;      // only j > i inside the diagonal word
+      for (int t = jmin; t < jmax; ++t) {
+        const float4 o = s_box[wave][t];
+        const float xx1 = fmaxf(bi.x, o.x), yy1 = fmaxf(bi.y, o.y);
+        const float xx2 = fminf(bi.z, o.z), yy2 = fminf(bi.w, o.w);
+        if (!full && (xx2 <= xx1 || yy2 <= yy1)) continue;   // disjoint: IoU 0 (or NaN), never > thr
+        const float ww = fmaxf(0.0f, xx2 - xx1), hh = fmaxf(0.0f, yy2 - yy1);
+        const float inter = ww * hh;
+        const float ovr = inter / (iarea + s_area[wave][t] - inter);
+        if (ovr > thr_f) bits |= 1ull << t;
+      }
+      if (i < n) mrow[(long)i * ws.words + w] = bits;
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+__global__ __launch_bounds__(1024) void nms_big_scan_kernel(int A, int nc, NmsWs ws) {
+  __shared__ unsigned long long s_or[16];
+  __shared__ int s_kept;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbig = ws.big[0];
+  for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
+    const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
+    const int n = ws.cls_cnt[(long)b * nc + c];
+    const int off = ws.cls_off[(long)b * nc + c];
+    const uint64_t* mrow = ws.mask + ((long)b * A + off) * ws.words;
+    int* idx = ws.scratch + (long)b * A + off;     // sorted anchor ids (input)
+    int* kept_pos = reinterpret_cast<int*>(ws.gboxes + (long)b * A + off);   // sorted positions kept
+    if (tid == 0) s_kept = 0;
+    __syncthreads();
+    const int W = (n + 63) >> 6;
+    for (int k = 0; k < W; ++k) {
+      const int nk = s_kept;
+      unsigned long long acc = 0;
+      for (int r = tid; r < nk; r += 1024) acc |= mrow[(long)kept_pos[r] * ws.words + k];
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) acc |= __shfl_xor(acc, o);
+      if (lane == 0) s_or[wave] = acc;
+      __syncthreads();
+      if (wave == 0) {
+        unsigned long long sup = 0;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sup |= s_or[q];
+        const int i = (k << 6) + lane;
+        const uint64_t diag = i < n ? mrow[(long)i * ws.words + k] : 0ull;
+        const int m = min(64, n - (k << 6));
+        unsigned long long alive = (m == 64 ? ~0ull : ((1ull << m) - 1ull)) & ~sup;
+        for (int t = 0; t < m; ++t) {
+          if ((alive >> t) & 1ull) alive &= ~__shfl(diag, t);
+        }
+        const int pos = nk + __popcll(alive & ((1ull << lane) - 1ull));
+        if ((alive >> lane) & 1ull) kept_pos[pos] = i;
+        if (lane == 0) s_kept = nk + __popcll(alive);
+      }
+      __syncthreads();
+    }
+    // kept sorted positions -> anchor ids, in score order (positions are increasing)
+    const int nk = s_kept;
+    for (int r = tid; r < nk; r += 1024) kept_pos[r] = idx[kept_pos[r]];   // own element only
+    __syncthreads();
+    for (int r = tid; r < nk; r += 1024) idx[r] = kept_pos[r];
+    __syncthreads();
+    if (tid == 0) ws.cls_cnt[(long)b * nc + c] = nk;
+    __syncthreads();
+  }
+}
+
 __global__ void nms_compact_kernel(int A, int nc, NmsWs ws, int64_t* keep_idx, int* keep_lbl,
                                    int* counts) {
   const int b = blockIdx.x;
@@ -299,6 +487,11 @@ static NmsWs carve(void* ws, int n, int A, int nc) {
   w.cls_cnt = (int*)p;
   p += r256((size_t)n * nc * 4);
   w.cls_off = (int*)p;
+  p += r256((size_t)n * nc * 4);
+  w.big = (int*)p;
+  p += r256((size_t)(1 + 2 * n * nc) * 4);
+  w.words = (A + 63) / 64;
+  w.mask = (uint64_t*)p;
   return w;
 }
 
@@ -342,7 +535,7 @@ yms_status yms_head_decode(int dtype, int n, int nc, int nlev, const void* const
   p.nlev = nlev; p.no_ld = no_ld; p.nc = nc; p.A = A; p.n = n; p.conf = conf;
   p.out = out; p.bxy = boxes_xyxy; p.score = nms_score; p.label = label;
   const long total = (long)n * A;
-  dim3 grid((unsigned)std::min<long>(cdiv(total, 256), 16384));
+  dim3 grid((unsigned)std::min<long>(cdiv(total, 16), 16384));
   hipStream_t st = (hipStream_t)stream;
   if (dtype == YMS_BF16) hipLaunchKernelGGL(head_decode_kernel<bf16>, grid, dim3(256), 0, st, p);
   else if (dtype == YMS_F16) hipLaunchKernelGGL(head_decode_kernel<f16>, grid, dim3(256), 0, st, p);
@@ -355,14 +548,15 @@ yms_status yms_nms_prep(int n, int A, int nc, const float* pred, float conf, flo
                         float* score, int* label, void* stream) {
   if (n <= 0 || A <= 0 || nc <= 0 || !pred || !boxes_xyxy || !score || !label) return YMS_ERR_INVALID;
   const long total = (long)n * A;
-  hipLaunchKernelGGL(nms_prep_kernel, dim3((unsigned)std::min<long>(cdiv(total, 256), 16384)), dim3(256), 0,
+  hipLaunchKernelGGL(nms_prep_kernel, dim3((unsigned)std::min<long>(cdiv(total, 16), 16384)), dim3(256), 0,
                      (hipStream_t)stream, n, A, nc, pred, conf, boxes_xyxy, score, label);
   return launch_status();
 }
 
 size_t yms_nms_ws_bytes(int n, int A, int nc) {
   return r256((size_t)n * A * 8) + r256((size_t)n * A * 16) + r256((size_t)n * A * 4) +
-         r256((size_t)n * nc * 4) + r256((size_t)n * nc * 4);
+         r256((size_t)n * nc * 4) + r256((size_t)n * nc * 4) + r256((size_t)(1 + 2 * n * nc) * 4) +
+         (size_t)n * A * ((A + 63) / 64) * 8;
 }
 
 yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, const float* score,
@@ -373,8 +567,28 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
   if ((uintptr_t)ws % 16 != 0 || (uintptr_t)boxes_xyxy % 16 != 0) return YMS_ERR_INVALID;
   NmsWs w = carve(ws, n, A, nc);
   hipStream_t st = (hipStream_t)stream;
-  hipLaunchKernelGGL(nms_class_kernel, dim3((unsigned)nc, (unsigned)n), dim3(256), 0, st, A, nc, boxes_xyxy,
-                     score, label, iou, w);
+  if (hipMemsetAsync(w.big, 0, 4, st) != hipSuccess) return YMS_ERR_LAUNCH;
+  hipLaunchKernelGGL(nms_bucket_kernel, dim3((unsigned)n), dim3(1024), (size_t)nc * 8, st, A, nc, score, label, w);
+  hipLaunchKernelGGL(nms_class_kernel, dim3((unsigned)nc, (unsigned)n), dim3(256), 0, st, A, nc, boxes_xyxy, iou, w);
+  static bool attr_set = false;
+  if (!attr_set) {
+    if (hipFuncSetAttribute((const void*)nms_big_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NMS_BIG_LDS_KEYS * 8) != hipSuccess)
+      return YMS_ERR_LAUNCH;
+    attr_set = true;
+  }
+  if (A > NMS_CAP) {
+    // float threshold with (float)x > thr_f  <=>  (double)x > iou  for every non-NaN float x
+    float thr_f = (float)iou;
+    if ((double)thr_f > iou) thr_f = nextafterf(thr_f, -INFINITY);
+    const int full = iou < 0.0 ? 1 : 0;
+    const unsigned segs = (unsigned)std::min(256, n * nc);
+    hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_BIG_LDS_KEYS * 8, st, A, nc,
+                       boxes_xyxy, w);
+    hipLaunchKernelGGL(nms_big_mask_kernel, dim3((unsigned)((A + 63) / 64), std::min(64u, segs)), dim3(256), 0, st,
+                       A, nc, thr_f, full, w);
+    hipLaunchKernelGGL(nms_big_scan_kernel, dim3(segs), dim3(1024), 0, st, A, nc, w);
+  }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
   hipLaunchKernelGGL(nms_compact_kernel, dim3((unsigned)n), dim3(256), 0, st, A, nc, w, keep_idx, keep_lbl,
