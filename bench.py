@@ -174,7 +174,8 @@ def main():
 
         log(f"[rank {rank}] train warmup {a.warmup} + {a.steps} steps, B={a.batch}/GPU")
         dt = timed(train_step, a.steps, a.warmup, world)
-        result["train"] = {"dt": dt, "img_s": world * a.batch * a.steps / dt}
+        result["train"] = {"dt": dt, "img_s": world * a.batch * a.steps / dt,
+                           "peak_gb": torch.cuda.max_memory_allocated() / 2**30}
         log(f"[rank {rank}] train: {result['train']['img_s']:.1f} img/s ({dt / a.steps * 1e3:.1f} ms/step)")
         if rank == 0 and not a.no_profile:
             _lib.profile_begin()
@@ -225,7 +226,8 @@ def main():
                               "parallelism": f"dp{world}",
                               "loss": "surrogate sum(mean(o^2)) over the 3 head maps (reference loss "
                                       "crashes for nc=80, SURVEY 0.5)",
-                              "conv_gflop_per_img_fwd": round(flops_img / 1e9, 3)}
+                              "conv_gflop_per_img_fwd": round(flops_img / 1e9, 3),
+                              "peak_hbm_gib": round(tr["peak_gb"], 2)}
             if "train_prof" in result:
                 line["roofline"] = conv_roofline(result["train_prof"], "conv implicit-GEMM fwd+dgrad+wgrad "
                                                  f"({a.dtype} MFMA), one training step")

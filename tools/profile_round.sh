@@ -1,0 +1,33 @@
+#!/bin/bash
+# Profile the bench command on a GPU box (run through gpurun from the repo root):
+#   tools/profile_round.sh r01
+# 1) rocprofv3 --kernel-trace --stats of the default bench (train + infer) -> per-kernel times
+# 2-4) separate PMC passes (FETCH_SIZE | WRITE_SIZE | MFMA busy) of a short bench run
+# Outputs under gpurun_out/<tag>/; copy the summaries into profiles/ afterwards.
+set -e
+TAG=${1:-r01}
+ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
+OUT=$ROOT/gpurun_out/$TAG
+mkdir -p "$OUT"
+cd /tmp && export TMPDIR=/tmp
+timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run -- \
+  python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
+echo "stats done"
+for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
+  d=$(echo "$c" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+  timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/$d" -o run -- \
+    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile > "$OUT/$d.json" 2> "$OUT/$d.err"
+  echo "pmc $c done"
+done
+# condense on the box (raw csvs can exceed gpurun's 64 MiB pull limit)
+set +e
+cd "$ROOT"
+for e in "$OUT"/*.err; do echo "== $e"; grep -v "^[EWI]2026\|^[EWI][0-9]\{8\}" "$e" | tail -5; done
+ls -la "$OUT"/*/ | head -40
+du -sh "$OUT"/* > "$OUT/sizes.txt" || true
+python3 tools/rocprof_summary.py stats "$OUT/stats/run_kernel_stats.csv" > "$OUT/stats_summary.txt"
+python3 tools/rocprof_summary.py pmc "$OUT/fetch_size/run_counter_collection.csv" \
+  "$OUT/write_size/run_counter_collection.csv" "$OUT/sq_valu_mfma_busy_cycles/run_counter_collection.csv" \
+  > "$OUT/pmc_summary.json"
+for f in $(find "$OUT" -name "*.csv" -size +4M); do head -c 200000 "$f" > "$f.head"; rm -f "$f"; done
+echo "summaries done"

@@ -1,0 +1,112 @@
+#!/usr/bin/env python3
+"""Condense rocprofv3 output of `bench.py` into the per-family summaries kept under profiles/.
+
+    python tools/rocprof_summary.py stats  <kernel_stats.csv>            > profiles/rNN_..._stats.txt
+    python tools/rocprof_summary.py pmc    <counter_collection.csv> ...  > profiles/rNN_..._traffic.json
+
+`stats`: the rocprofv3 --kernel-trace --stats table regrouped by kernel family.  The conv
+families are the ones bench.py's roofline aggregates (yms_conv_fwd / _dgrad / _wgrad calls):
+  conv_nt MODE 0  -> yms_conv_fwd   (one launch per call)
+  conv_nt MODE 1/2-> yms_conv_dgrad (one launch per call; MODE 2 = stride-2 parity classes)
+  conv_wgrad + wgrad_reduce -> yms_conv_wgrad (one or two launches per call)
+so "avg us per conv call" here is directly comparable with bench.py's roofline.avg_launch_us.
+
+`pmc`: per-dispatch FETCH_SIZE / WRITE_SIZE (KB; collected in separate passes since they
+do not fit one TCC pass on gfx950) and SQ_VALU_MFMA_BUSY_CYCLES / GRBM_GUI_ACTIVE, averaged
+per family.  HBM bytes per launch = (2 * FETCH_SIZE + WRITE_SIZE) * 1024: on gfx950
+FETCH_SIZE tallies 128-B requests of 16-B/lane streaming loads at 64 B
+(MI355X_MICROARCH.md "HBM [CDNA4]").  Infinity-Cache (256 MiB) hits are counted by the
+fabric-side counters, i.e. this is "bytes below L2", an upper bound on HBM bytes.
+"""
+import csv
+import json
+import re
+import sys
+from collections import defaultdict
+
+
+def family(name):
+    m = re.search(r"conv_nt_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)E", name)
+    if m:
+        return "conv_fwd" if int(m.group(3)) == 0 else "conv_dgrad"
+    m = re.search(r"conv_nt_kernel<(.*)>", name)
+    if m:   # demangled: <T, KS, MODE, EPI, BM, BN, WGM, WGN>; count from the end (T/KS demangle oddly)
+        mode = int(m.group(1).split(",")[-6])
+        return "conv_fwd" if mode == 0 else "conv_dgrad"
+    if "conv_wgrad_kernel" in name or "wgrad_reduce_kernel" in name:
+        return "conv_wgrad"
+    m = re.search(r"yms::(\w+?)(?:_kernel)?[(<]", name) or re.search(r"_ZN3yms\d+(\w+?)(?:_kernel)?I", name) \
+        or re.search(r"N3yms\d+(\w+)E", name)
+    if m:
+        return m.group(1)
+    return name[:48]
+
+
+def is_call_head(name):
+    """Kernels that start one yms_conv_* call (the wgrad reducer does not)."""
+    return "conv_nt_kernel" in name or "conv_wgrad_kernel" in name
+
+
+def stats(path):
+    fam = defaultdict(lambda: [0, 0.0, 0])   # launches, total ns, call heads
+    for r in csv.DictReader(open(path)):
+        f = family(r["Name"])
+        fam[f][0] += int(r["Calls"])
+        fam[f][1] += float(r["TotalDurationNs"])
+        if is_call_head(r["Name"]):
+            fam[f][2] += int(r["Calls"])
+    tot = sum(v[1] for v in fam.values())
+    print(f"# rocprofv3 --kernel-trace --stats, regrouped by family ({path})")
+    print(f"{'family':28s} {'launches':>9s} {'total_ms':>10s} {'avg_us':>9s} {'pct':>6s}")
+    for f, (n, ns, _) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
+        print(f"{f:28s} {n:9d} {ns / 1e6:10.3f} {ns / n / 1e3:9.2f} {100 * ns / tot:6.2f}")
+    conv = [fam[k] for k in ("conv_fwd", "conv_dgrad", "conv_wgrad") if k in fam]
+    calls = sum(v[2] for v in conv)
+    ns = sum(v[1] for v in conv)
+    if calls:
+        print(f"\nconv calls (fwd+dgrad+wgrad): {calls}, {ns / 1e6:.3f} ms, avg {ns / calls / 1e3:.2f} us per call")
+        for k in ("conv_fwd", "conv_dgrad", "conv_wgrad"):
+            if k in fam and fam[k][2]:
+                print(f"  {k:12s} calls {fam[k][2]:6d}  avg {fam[k][1] / fam[k][2] / 1e3:8.2f} us per call")
+
+
+def pmc(paths):
+    # per dispatch: counter -> value (rocprofv3 may emit one row per counter per dispatch)
+    per = defaultdict(dict)
+    names = {}
+    for p in paths:
+        tag = p
+        for r in csv.DictReader(open(p)):
+            did = (tag, r.get("Dispatch_Id") or r.get("Correlation_Id"))
+            names[did] = r["Kernel_Name"]
+            per[did][r["Counter_Name"]] = per[did].get(r["Counter_Name"], 0.0) + float(r["Counter_Value"])
+    fam = defaultdict(lambda: defaultdict(list))
+    for did, cv in per.items():
+        f = family(names[did])
+        for c, v in cv.items():
+            fam[f][c].append(v)
+    out = {}
+    for f, cs in fam.items():
+        d = {c: sum(v) / len(v) for c, v in cs.items()}
+        d["dispatches"] = {c: len(v) for c, v in cs.items()}
+        if "FETCH_SIZE" in d and "WRITE_SIZE" in d:
+            d["hbm_bytes_per_launch"] = (2.0 * d["FETCH_SIZE"] + d["WRITE_SIZE"]) * 1024.0
+        out[f] = d
+    conv = [f for f in ("conv_fwd", "conv_dgrad", "conv_wgrad") if f in out and "hbm_bytes_per_launch" in out[f]]
+    if conv:
+        # per conv *call*: wgrad calls launch kernel + reducer; weight by head launches
+        tot_b = sum(out[f]["hbm_bytes_per_launch"] * out[f]["dispatches"]["FETCH_SIZE"] for f in conv)
+        heads = 0
+        for did, nm in names.items():
+            if is_call_head(nm) and "FETCH_SIZE" in per[did]:
+                heads += 1
+        out["_conv_all"] = {"calls": heads, "hbm_bytes_per_call": tot_b / max(heads, 1)}
+    json.dump(out, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+if __name__ == "__main__":
+    if sys.argv[1] == "stats":
+        stats(sys.argv[2])
+    else:
+        pmc(sys.argv[2:])
