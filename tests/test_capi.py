@@ -36,8 +36,9 @@ def test_version_and_status():
 def test_host_shape_validation_and_sizes():
     sh = L.ConvShape(2, 64, 64, 32, 64, 3, 2, 1, 32, 32, L.BF16)
     sp = ctypes.pointer(sh)
-    # packed weights: cout padded to 128 rows, K = 9 taps x 32 ch padded to 32-element tiles
-    assert L.lib().yms_conv_packed_elems(sp, 0) == 128 * 9 * 32
+    # packed weights: cout padded to 128 rows, K = 9 taps x 32 ch = 288 padded to the
+    # 128-byte (64 bf16) K tile of the NT kernel -> 320
+    assert L.lib().yms_conv_packed_elems(sp, 0) == 128 * 320
     assert L.lib().yms_conv_stats_ld(sp) == 128
     assert L.lib().yms_conv_stats_rows(sp) > 0
     assert L.lib().yms_conv_wgrad_ws_bytes(sp) > 0
