@@ -70,6 +70,16 @@ def timed(fn, steps, warmup, world):
     return dt
 
 
+def add_traffic(roof, mode, workload):
+    t, src, busy = pmc_traffic(mode, workload)
+    if t is not None:
+        roof["traffic"] = round(t)
+        roof["traffic_unit"] = "bytes below L2 per conv launch (PMC)"
+        roof["traffic_source"] = src
+        if busy is not None:
+            roof["mfma_busy_frac_pmc"] = round(busy, 4)
+
+
 def conv_roofline(prof, label):
     calls = sum(v[0] for k, v in prof.items() if k.startswith("yms_conv_") and v[2])
     ms = sum(v[1] for k, v in prof.items() if k.startswith("yms_conv_") and v[2])
@@ -79,6 +89,23 @@ def conv_roofline(prof, label):
             "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None, "kernel": label,
             "launches": calls, "avg_launch_us": round(ms * 1e3 / max(calls, 1), 2),
             "algorithmic_gflop_per_launch": round(fl / max(calls, 1) / 1e9, 3)}
+
+
+def pmc_traffic(mode, workload):
+    """HBM bytes per conv call from the newest committed PMC profile of the same workload
+    (profiles/*_pmc_traffic.json, written by tools/profile_round.sh + tools/rocprof_summary.py
+    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this script).  PMC
+    counters cannot be read from inside the timed run, so this is the profiled value of the
+    same command; None when no profile of this exact workload exists."""
+    import glob
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
+        try:
+            d = json.load(open(f)).get(mode, {})
+        except Exception:
+            continue
+        if d.get("bench_config", {}).get("workload") == workload and "conv_hbm_bytes_per_call" in d:
+            return d["conv_hbm_bytes_per_call"], os.path.relpath(f, ROOT), d.get("conv_mfma_busy_frac")
+    return None, None, None
 
 
 def cpu_baseline_train(version, nc, size, batch=4, steps=4):
@@ -231,6 +258,7 @@ def main():
             if "train_prof" in result:
                 line["roofline"] = conv_roofline(result["train_prof"], "conv implicit-GEMM fwd+dgrad+wgrad "
                                                  f"({a.dtype} MFMA), one training step")
+                add_traffic(line["roofline"], "train", line["config"]["workload"])
         if "infer" in result:
             inf = {"value": round(result["infer"]["img_s"], 2), "unit": "images/sec",
                    "ms_per_batch": round(result["infer"]["dt"] / a.steps * 1e3, 3),
@@ -238,6 +266,7 @@ def main():
                                "(forward + decode + class-wise NMS)"}
             if "infer_prof" in result:
                 inf["roofline"] = conv_roofline(result["infer_prof"], f"conv implicit-GEMM fwd ({a.dtype} MFMA)")
+                add_traffic(inf["roofline"], "infer", inf["workload"])
             line["infer"] = inf
             if "value" not in line:
                 line["value"] = inf["value"]

@@ -92,8 +92,9 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
 yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float* rmean,
                        const float* rvar, float eps, float* scale, float* shift, void* stream);
 /* Train: reduce partial stats of `count` pixels -> mean/invstd, scale/shift, and update the
- * running buffers (unbiased var, momentum) exactly like nn.BatchNorm2d.  mean_invstd: [2][c]. */
-yms_status yms_bn_finalize(int c, const float* stats, int rows, int stats_ld, long count,
+ * running buffers (unbiased var, momentum) exactly like nn.BatchNorm2d.  mean_invstd: [2][c].
+ * The stats table is consumed: long tables are pre-reduced in place. */
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream);

@@ -10,14 +10,18 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/stats" -o run -- \
+timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- \
   python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
 echo "stats done"
-for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
-  d=$(echo "$c" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
-  timeout -k 10 600 rocprofv3 --pmc $c -d "$OUT/$d" -o run -- \
-    python3 "$ROOT/bench.py" --steps 2 --warmup 1 --no-cpu-baseline --no-profile > "$OUT/$d.json" 2> "$OUT/$d.err"
-  echo "pmc $c done"
+# PMC passes per mode (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950)
+for mode in train infer; do
+  for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
+    d=pmc_${mode}_$(echo "$c" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
+    timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/$d" -o run -- \
+      python3 "$ROOT/bench.py" --mode $mode --steps 2 --warmup 1 --no-cpu-baseline --no-profile \
+      > "$OUT/$d.json" 2> "$OUT/$d.err"
+    echo "pmc $mode $c done"
+  done
 done
 # condense on the box (raw csvs can exceed gpurun's 64 MiB pull limit)
 set +e
@@ -26,8 +30,7 @@ for e in "$OUT"/*.err; do echo "== $e"; grep -v "^[EWI]2026\|^[EWI][0-9]\{8\}" "
 ls -la "$OUT"/*/ | head -40
 du -sh "$OUT"/* > "$OUT/sizes.txt" || true
 python3 tools/rocprof_summary.py stats "$OUT/stats/run_kernel_stats.csv" > "$OUT/stats_summary.txt"
-python3 tools/rocprof_summary.py pmc "$OUT/fetch_size/run_counter_collection.csv" \
-  "$OUT/write_size/run_counter_collection.csv" "$OUT/sq_valu_mfma_busy_cycles/run_counter_collection.csv" \
-  > "$OUT/pmc_summary.json"
+python3 tools/rocprof_summary.py traffic "$OUT" > "$OUT/pmc_traffic.json"
+find "$OUT" -name "*.db" -delete
 for f in $(find "$OUT" -name "*.csv" -size +4M); do head -c 200000 "$f" > "$f.head"; rm -f "$f"; done
 echo "summaries done"

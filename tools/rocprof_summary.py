@@ -26,13 +26,15 @@ from collections import defaultdict
 
 
 def family(name):
-    m = re.search(r"conv_nt_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)E", name)
+    # conv_nt_kernel<T, KS, MODE, EPI, BM, BN, WGM, WGN>: EPI 0 (affine) / 1 (BN stats) are
+    # forward launches, 2 (store) / 3 (accumulate) are dgrad launches
+    m = re.search(r"conv_nt_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
     if m:
-        return "conv_fwd" if int(m.group(3)) == 0 else "conv_dgrad"
+        return "conv_fwd" if int(m.group(4)) <= 1 else "conv_dgrad"
     m = re.search(r"conv_nt_kernel<(.*)>", name)
-    if m:   # demangled: <T, KS, MODE, EPI, BM, BN, WGM, WGN>; count from the end (T/KS demangle oddly)
-        mode = int(m.group(1).split(",")[-6])
-        return "conv_fwd" if mode == 0 else "conv_dgrad"
+    if m:   # demangled (rocprof mangles T/KS oddly): count from the end
+        epi = int(m.group(1).split(",")[-5])
+        return "conv_fwd" if epi <= 1 else "conv_dgrad"
     if "conv_wgrad_kernel" in name or "wgrad_reduce_kernel" in name:
         return "conv_wgrad"
     m = re.search(r"yms::(\w+?)(?:_kernel)?[(<]", name) or re.search(r"_ZN3yms\d+(\w+?)(?:_kernel)?I", name) \
@@ -71,6 +73,46 @@ def stats(path):
 
 
 def pmc(paths):
+    json.dump(pmc_families(paths), sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+def traffic(out_dir):
+    """profile_round.sh output dir -> {mode: {families, conv_hbm_bytes_per_call, ...}}."""
+    import os
+    res = {"source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE "
+                     "SQ_BUSY_CYCLES, separate passes of `bench.py --mode M --steps 2 --warmup 1`; "
+                     "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 half-counted 128-B reads)"}
+    for mode in ("train", "infer"):
+        paths = [os.path.join(out_dir, f"pmc_{mode}_{c}", "run_counter_collection.csv")
+                 for c in ("fetch_size", "write_size", "sq_valu_mfma_busy_cycles")]
+        paths = [p for p in paths if os.path.exists(p)]
+        if not paths:
+            continue
+        fam = pmc_families(paths)
+        d = {"families": fam}
+        if "_conv_all" in fam:
+            d["conv_hbm_bytes_per_call"] = fam["_conv_all"]["hbm_bytes_per_call"]
+        busy = sum(fam[f].get("SQ_VALU_MFMA_BUSY_CYCLES", 0) * fam[f]["dispatches"].get("SQ_VALU_MFMA_BUSY_CYCLES", 0)
+                   for f in ("conv_fwd", "conv_dgrad", "conv_wgrad") if f in fam)
+        act = sum(fam[f].get("GRBM_GUI_ACTIVE", 0) * fam[f]["dispatches"].get("GRBM_GUI_ACTIVE", 0)
+                  for f in ("conv_fwd", "conv_dgrad", "conv_wgrad") if f in fam)
+        if act:
+            # GRBM_GUI_ACTIVE sums the 8 XCDs; MFMA busy sums 1024 SIMDs (32 per 32x32x16 MFMA)
+            d["conv_mfma_busy_frac"] = busy / (act / 8.0 * 1024.0)
+        jf = os.path.join(out_dir, f"pmc_{mode}_fetch_size.json")
+        try:
+            line = json.loads(open(jf).read().strip().splitlines()[-1])
+            cfg = line.get("config", {})
+            d["bench_config"] = {"workload": cfg.get("workload"), "dtype": line.get("dtype")}
+        except Exception:
+            pass
+        res[mode] = d
+    json.dump(res, sys.stdout, indent=1, sort_keys=True)
+    print()
+
+
+def pmc_families(paths):
     # per dispatch: counter -> value (rocprofv3 may emit one row per counter per dispatch)
     per = defaultdict(dict)
     names = {}
@@ -101,12 +143,13 @@ def pmc(paths):
             if is_call_head(nm) and "FETCH_SIZE" in per[did]:
                 heads += 1
         out["_conv_all"] = {"calls": heads, "hbm_bytes_per_call": tot_b / max(heads, 1)}
-    json.dump(out, sys.stdout, indent=1, sort_keys=True)
-    print()
+    return out
 
 
 if __name__ == "__main__":
     if sys.argv[1] == "stats":
         stats(sys.argv[2])
+    elif sys.argv[1] == "traffic":
+        traffic(sys.argv[2])
     else:
         pmc(sys.argv[2:])

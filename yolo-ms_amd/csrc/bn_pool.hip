@@ -39,7 +39,41 @@ __global__ void bn_fold_kernel(int c, const float* g, const float* b, const floa
 
 // stats: [rows][2][ld]; 32 channels x 32 row-lanes per block (1024 threads), 4 independent
 // fp64 accumulators per lane so the row loop is load-throughput, not latency, bound.
-__global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* stats, int rows, int ld,
+// Pre-reduction for long statistics tables (one row per conv M tile): block (cb, s) sums rows
+// [s*R, (s+1)*R) of channels [64cb, 64cb+64) in fp64 and stores the sum over row s*R -- the
+// first row of its own range, so no block reads a row another block writes.
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int c, float* stats, int rows, int ld, int R) {
+  __shared__ double red[2][4][64];
+  const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
+  const int ch = blockIdx.x * 64 + tx;
+  const int r0 = blockIdx.y * R, r1 = min(rows, r0 + R);
+  double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
+  if (ch < c) {
+    int r = r0 + ty;
+    for (; r + 4 < r1; r += 8) {
+      a1 += stats[(long)r * 2 * ld + ch];
+      a2 += stats[(long)r * 2 * ld + ld + ch];
+      b1 += stats[(long)(r + 4) * 2 * ld + ch];
+      b2 += stats[(long)(r + 4) * 2 * ld + ld + ch];
+    }
+    if (r < r1) {
+      a1 += stats[(long)r * 2 * ld + ch];
+      a2 += stats[(long)r * 2 * ld + ld + ch];
+    }
+  }
+  red[0][ty][tx] = a1 + b1;
+  red[1][ty][tx] = a2 + b2;
+  __syncthreads();
+  if (ty == 0 && ch < c) {
+    const double t1 = (red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]);
+    const double t2 = (red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]);
+    stats[(long)r0 * 2 * ld + ch] = (float)t1;
+    stats[(long)r0 * 2 * ld + ld + ch] = (float)t2;
+  }
+}
+
+// rows are read at stride rs (rs > 1 after bn_stats_partial_kernel)
+__global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* stats, int rows, int ld, int rs,
                                                            long count, const float* g, const float* b,
                                                            float* rm, float* rv, float momentum, float eps,
                                                            float* mi, float* scale, float* shift) {
@@ -52,13 +86,13 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* s
     for (; r + 96 < rows; r += 128) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a1[u] += stats[(long)(r + 32 * u) * 2 * ld + ch];
-        a2[u] += stats[(long)(r + 32 * u) * 2 * ld + ld + ch];
+        a1[u] += stats[(long)(r + 32 * u) * rs * 2 * ld + ch];
+        a2[u] += stats[(long)(r + 32 * u) * rs * 2 * ld + ld + ch];
       }
     }
     for (; r < rows; r += 32) {
-      a1[0] += stats[(long)r * 2 * ld + ch];
-      a2[0] += stats[(long)r * 2 * ld + ld + ch];
+      a1[0] += stats[(long)r * rs * 2 * ld + ch];
+      a2[0] += stats[(long)r * rs * 2 * ld + ld + ch];
     }
   }
   red[0][ty][tx] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
@@ -106,6 +140,10 @@ __device__ __forceinline__ void load_params8(const float* p, int c0, int c, floa
   for (int i = 0; i < 8; ++i) v[i] = (p && c0 + i < c) ? p[c0 + i] : dflt;
 }
 
+// U pixels per thread per iteration: all U loads issue before any use (memory-level
+// parallelism; these kernels are HBM-bound).
+constexpr int BN_U = 4;
+
 template <typename T>
 __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const T* z, int z_ld, int z_off,
                                                          const float* scale, const float* shift, int act,
@@ -118,18 +156,33 @@ __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const
   load_params8(scale, c0, c, sc, 1.0f);
   load_params8(shift, c0, c, sh, 0.0f);
   const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-  for (long pix = p0 + m.py; pix < p1; pix += m.PY) {
-    float v[8], r[8];
-    load8(z + pix * z_ld + z_off + c0, nv, v);
-    if (res) load8(res + pix * res_ld + res_off + c0, nv, r);
+  for (long base = p0 + m.py; base < p1; base += (long)m.PY * BN_U) {
+    Raw8<T> zr[BN_U], rr[BN_U];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      float a = v[i] * sc[i] + sh[i];
-      if (act == YMS_ACT_SILU) a = silu_f(a);
-      if (res) a += r[i];
-      v[i] = a;
+    for (int u = 0; u < BN_U; ++u) {
+      const long pix = base + (long)u * m.PY;
+      if (pix < p1) {
+        load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
+        if (res) load_raw8(res + pix * res_ld + res_off + c0, nv, rr[u]);
+      }
     }
-    store8(y + pix * y_ld + y_off + c0, nv, v);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long pix = base + (long)u * m.PY;
+      if (pix < p1) {
+        float v[8], r[8];
+        unpack8(zr[u], v);
+        if (res) unpack8(rr[u], r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float a = v[i] * sc[i] + sh[i];
+          if (act == YMS_ACT_SILU) a = silu_f(a);
+          if (res) a += r[i];
+          v[i] = a;
+        }
+        store8(y + pix * y_ld + y_off + c0, nv, v);
+      }
+    }
   }
 }
 
@@ -157,23 +210,35 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
       load_params8(mi + c, c0, c, is, 0.f);
     }
     const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-    for (long pix = p0 + m.py; pix < p1; pix += m.PY) {
-      float gv[8], zv[8];
-      load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
-      if (HAS_Z) load8(z + pix * z_ld + z_off + c0, nv, zv);
+    for (long base = p0 + m.py; base < p1; base += (long)m.PY * BN_U) {
+      Raw8<T> gr[BN_U], zr[BN_U];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float da = gv[i], xh = 0.f;
-        if (HAS_Z) {
-          const float a = zv[i] * sc[i] + sh[i];
-          if (act == YMS_ACT_SILU) {
-            const float s = sigmoid_f(a);
-            da = gv[i] * (s * (1.0f + a * (1.0f - s)));
-          }
-          xh = (zv[i] - mu[i]) * is[i];
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = base + (long)u * m.PY;
+        if (pix < p1) {
+          load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
+          if (HAS_Z) load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
         }
-        a1[i] += da;
-        a2[i] += da * xh;
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = base + (long)u * m.PY;
+        if (pix < p1) {
+          float gv[8], zv[8];
+          unpack8(gr[u], gv);
+          if (HAS_Z) unpack8(zr[u], zv);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) {
+            float da = gv[i], xh = 0.f;
+            if (HAS_Z) {
+              const float a = zv[i] * sc[i] + sh[i];
+              if (act == YMS_ACT_SILU) da = gv[i] * dsilu_f(a);
+              xh = (zv[i] - mu[i]) * is[i];
+            }
+            a1[i] += da;
+            a2[i] += da * xh;
+          }
+        }
       }
     }
   }
@@ -249,42 +314,61 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
   ChanMap m(c);
   if (!m.active) return;
   const int c0 = m.g * 8, nv = min(8, c - c0);
-  float sc[8], sh[8], mu[8], is[8], k0[8], k1[8];
-  load_params8(scale, c0, c, sc, 0.f);
-  load_params8(shift, c0, c, sh, 0.f);
-  load_params8(mi, c0, c, mu, 0.f);
-  load_params8(mi + c, c0, c, is, 0.f);
-  load_params8(coef, c0, c, k0, 0.f);
-  load_params8(coef + c, c0, c, k1, 0.f);
-  const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-  for (long pix = p0 + m.py; pix < p1; pix += m.PY) {
-    float gv[8], zv[8], out[8];
-    load8(gy + pix * gy_ld + gy_off + c0, nv, gv);
-    load8(z + pix * z_ld + z_off + c0, nv, zv);
+  // dz = sc*(da - k0 - (z-mu)*is*k1) = sc*da + A + B*z
+  float sc[8], sh[8], A[8], Bz[8];
+  {
+    float mu[8], is[8], k0[8], k1[8];
+    load_params8(scale, c0, c, sc, 0.f);
+    load_params8(shift, c0, c, sh, 0.f);
+    load_params8(mi, c0, c, mu, 0.f);
+    load_params8(mi + c, c0, c, is, 0.f);
+    load_params8(coef, c0, c, k0, 0.f);
+    load_params8(coef + c, c0, c, k1, 0.f);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const float a = zv[i] * sc[i] + sh[i];
-      float da = gv[i];
-      if (act == YMS_ACT_SILU) {
-        const float s = sigmoid_f(a);
-        da = gv[i] * (s * (1.0f + a * (1.0f - s)));
-      }
-      const float xh = (zv[i] - mu[i]) * is[i];
-      out[i] = sc[i] * (da - k0[i] - xh * k1[i]);
+      Bz[i] = -sc[i] * k1[i] * is[i];
+      A[i] = -sc[i] * k0[i] - Bz[i] * mu[i];
     }
-    if (gres) {
-      float r[8];
-      if (gres_acc) {
-        load8(gres + pix * gres_ld + gres_off + c0, nv, r);
+  }
+  const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
+  for (long base = p0 + m.py; base < p1; base += (long)m.PY * BN_U) {
+    Raw8<T> gr[BN_U], zr[BN_U], rr[BN_U];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] += gv[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) r[i] = gv[i];
+    for (int u = 0; u < BN_U; ++u) {
+      const long pix = base + (long)u * m.PY;
+      if (pix < p1) {
+        load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
+        load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
+        if (gres && gres_acc) load_raw8(gres + pix * gres_ld + gres_off + c0, nv, rr[u]);
       }
-      store8(gres + pix * gres_ld + gres_off + c0, nv, r);
     }
-    store8(dz + pix * dz_ld + dz_off + c0, nv, out);
+#pragma unroll
+    for (int u = 0; u < BN_U; ++u) {
+      const long pix = base + (long)u * m.PY;
+      if (pix < p1) {
+        float gv[8], zv[8], out[8];
+        unpack8(gr[u], gv);
+        unpack8(zr[u], zv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          float da = gv[i];
+          if (act == YMS_ACT_SILU) da *= dsilu_f(zv[i] * sc[i] + sh[i]);
+          out[i] = sc[i] * da + A[i] + Bz[i] * zv[i];
+        }
+        if (gres) {
+          float r[8];
+          if (gres_acc) {
+            unpack8(rr[u], r);
+#pragma unroll
+            for (int i = 0; i < 8; ++i) r[i] += gv[i];
+            store8(gres + pix * gres_ld + gres_off + c0, nv, r);
+          } else {
+            store8(gres + pix * gres_ld + gres_off + c0, nv, gv);
+          }
+        }
+        store8(dz + pix * dz_ld + dz_off + c0, nv, out);
+      }
+    }
   }
 }
 
@@ -564,20 +648,32 @@ yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float
   return launch_status();
 }
 
-yms_status yms_bn_finalize(int c, const float* stats, int rows, int stats_ld, long count,
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream) {
   if (c <= 0 || !stats || rows <= 0 || count <= 0 || !gamma || !beta || !mean_invstd || !scale || !shift)
     return YMS_ERR_INVALID;
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, stats,
-                     rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps, mean_invstd, scale,
-                     shift);
+  if (stats_ld < c) return YMS_ERR_INVALID;
+  int rs = 1, nrows = rows;
+  if (rows > 256) {   // long tables: pre-reduce in parallel (in place), then finalize the partial rows
+    const int S = std::min(256, cdiv(rows, 64));
+    rs = cdiv(rows, S);
+    nrows = cdiv(rows, rs);
+    hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(cdiv(c, 64), nrows), dim3(256), 0, (hipStream_t)stream, c,
+                       stats, rows, stats_ld, rs);
+  }
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c,
+                     (const float*)stats, nrows, stats_ld, rs, count, gamma, beta, rmean, rvar, momentum, eps,
+                     mean_invstd, scale, shift);
   return launch_status();
 }
 
-static long elem_ppb(long npix) {
-  const long blocks = std::min<long>(std::max<long>((npix + 63) / 64, 1), 4096);
+// pixels per block for the channel-stationary kernels: about two U-pixel iterations per
+// thread, at most 8192 blocks
+static long elem_ppb(long npix, int c) {
+  const long py = 256 / ((c + 7) / 8);
+  const long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * 2), 1), 8192);
   return (npix + blocks - 1) / blocks;
 }
 
@@ -588,7 +684,7 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   if (npix <= 0 || !z || !y || !vok(z_ld, z_off, c) || !vok(y_ld, y_off, c)) return YMS_ERR_INVALID;
   if (res && !vok(res_ld, res_off, c)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = elem_ppb(npix);
+  const long ppb = elem_ppb(npix, c);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
   YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(affine_act_kernel<T>, dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
@@ -599,7 +695,7 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
 
 int yms_bn_bwd_rows(long npix) {
   if (npix <= 0) return 0;
-  long rows = (npix + 255) / 256;
+  long rows = (npix + 63) / 64;
   if (rows > 1024) rows = 1024;
   return (int)rows;
 }
@@ -649,7 +745,7 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
   if (!vok(z_ld, z_off, c) || !vok(gy_ld, gy_off, c) || !vok(dz_ld, dz_off, c)) return YMS_ERR_INVALID;
   if (gres && !vok(gres_ld, gres_off, c)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = elem_ppb(npix);
+  const long ppb = elem_ppb(npix, c);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
   YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,

@@ -57,6 +57,19 @@ struct NTParams {
   FastDiv cls_div_w[4], cls_div_hw[4];
 };
 
+// 16-B zero chunk: out-of-image / out-of-K im2col lanes load from here, so the A loads are
+// branch-free (no exec-masked regions around each global load).
+__device__ __attribute__((aligned(64))) u32x4 g_zero_chunk[4];
+
+// XCD-aware block order: hardware dispatches consecutive workgroup ids round-robin over the
+// 8 XCDs; remap (bijectively) so that consecutive LOGICAL ids -- the N tiles of one row
+// tile, and neighbouring row tiles that share im2col halo rows -- run on the same XCD and
+// share its L2 (MI355X_MICROARCH.md, Workgroup dispatch).
+__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
+  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7, k = orig >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
+}
+
 template <typename T> struct Mfma;
 template <> struct Mfma<bf16> {
   static __device__ __forceinline__ f32x16 mma(const u32x4& a, const u32x4& b, f32x16 c) {
@@ -71,7 +84,30 @@ template <> struct Mfma<f16> {
   }
 };
 
-template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN>
+// s_waitcnt vmcnt(N) alone (expcnt/lgkmcnt left at their maxima), gfx9 encoding
+template <int N> __device__ __forceinline__ void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
+}
+// workgroup barrier that does NOT drain the vector-memory counter (so LDS-DMA loads of later
+// k-tiles stay in flight across it); the clobbers keep the compiler from moving LDS accesses
+// across it.
+__device__ __forceinline__ void raw_barrier() {
+  asm volatile("" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
+}
+__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
+  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
+                                   (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0, 0);
+}
+
+// 16-bit types (GL): k-tiles are staged global->LDS directly with global_load_lds_dwordx4 into
+// an ST-deep ring of unpadded 128-B rows; 16-B chunk c of row r lives in slot
+// c ^ ((r >> 1) & 7) (conflict-free ds_read_b128 for 16 consecutive rows), which is realised
+// by swizzling each lane's global SOURCE address since the LDS image of one wave-instruction is
+// lane-linear.  The wait for k-tile kt is a counted vmcnt that leaves ST-2 later tiles in
+// flight across a raw s_barrier.  fp32 keeps the register-staged double buffer.
+template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST>
 __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -79,16 +115,21 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
   constexpr int A_SLOTS = BM / RSTEP;
   constexpr int B_CHUNKS = BN * NT_KCH;
   constexpr int B_SLOTS = (B_CHUNKS + 255) / 256;
-  constexpr int TILE_BYTES = (BM + BN) * NT_ROWP;
-  constexpr int EPI_P = BN + 4;                            // fp32 staging pitch (floats)
-  constexpr int SMEM = (2 * TILE_BYTES > BM * EPI_P * 4) ? 2 * TILE_BYTES : BM * EPI_P * 4;
   constexpr bool F32 = sizeof(T) == 4;
+  constexpr bool GL = !F32;
+  constexpr int PITCH = GL ? 128 : NT_ROWP;
+  constexpr int NSTAGE = GL ? ST : 2;
+  constexpr int TILE_BYTES = (BM + BN) * PITCH;
+  constexpr int EPI_P = BN + 4;                            // fp32 staging pitch (floats)
+  constexpr int SMEM = (NSTAGE * TILE_BYTES > BM * EPI_P * 4) ? NSTAGE * TILE_BYTES : BM * EPI_P * 4;
+  static_assert(!GL || B_CHUNKS % 256 == 0, "GL loader needs whole B passes");
   static_assert(TM >= 1 && TN >= 1 && A_SLOTS >= 1, "bad tile");
   __shared__ __attribute__((aligned(16))) char smem[SMEM];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int tile_n = blockIdx.x % p.tiles_n, tile_m = blockIdx.x / p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = wg % p.tiles_n, tile_m = wg / p.tiles_n;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   int M = p.M, nkt = p.nkt, Kc = p.Kc, ntx = 1, cls = 0;
   const char* wp = p.wp;
@@ -106,81 +147,89 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
   }
 
   // ---- im2col loader state (A side): fixed chunk column q, rows r0 + RSTEP*i ----
-  const int q = tid & (NT_KCH - 1), r0 = tid / NT_KCH;
-  int a_base[A_SLOTS], a_y[A_SLOTS], a_x[A_SLOTS];
-  bool a_ok[A_SLOTS];
+  // (GL: the thread fills LDS slot tid&7 of rows r0 + 32i, i.e. chunk (tid&7) ^ ((tid>>4)&7))
+  const int q = GL ? ((tid & 7) ^ ((tid >> 4) & 7)) : (tid & (NT_KCH - 1)), r0 = tid / NT_KCH;
+  // Per row slot: the element offset of its tap-(0,0) source pixel (32-bit; the host checks
+  // the source fits) and a bit mask of the taps that land inside the image.  Per k-tile the
+  // A address is then offset + delta(tap) + channel chunk, with no per-tap bounds arithmetic.
+  // Tap t displaces the source pixel by (dy, dx): forward (+t/KS, +t%KS); stride-1 dgrad
+  // (-t/KS, -t%KS); stride-2 dgrad parity class (-jy, -jx).
+  constexpr int NTAPS = MODE == MODE_DGRAD2 ? 4 : KS * KS;
+  constexpr int SGN = MODE == MODE_FWD ? 1 : -1;
+  auto tap_dyx = [&](int t, int& dy, int& dx) {
+    if (MODE == MODE_DGRAD2) {
+      dy = ntx == 1 ? t : (t >> 1);
+      dx = ntx == 1 ? 0 : (t & 1);
+    } else {
+      dy = t / KS;
+      dx = t - (t / KS) * KS;
+    }
+  };
+  int a_off[A_SLOTS];
+  uint32_t a_msk[A_SLOTS];
 #pragma unroll
   for (int i = 0; i < A_SLOTS; ++i) {
     const int m = m0 + r0 + RSTEP * i;
-    a_ok[i] = m < M;
-    const uint32_t mm = a_ok[i] ? (uint32_t)m : 0u;
+    const bool row_ok = m < M;
+    const uint32_t mm = row_ok ? (uint32_t)m : 0u;
     const uint32_t n = fdiv(mm, dv_hw);
     const uint32_t rem = mm - n * dv_hw.d;
     const uint32_t oy = fdiv(rem, dv_w);
     const uint32_t ox = rem - oy * dv_w.d;
-    a_base[i] = (int)n * p.SH;
+    int y0, x0;
     if (MODE == MODE_FWD) {
-      a_y[i] = (int)oy * p.stride - p.pad;
-      a_x[i] = (int)ox * p.stride - p.pad;
+      y0 = (int)oy * p.stride - p.pad;
+      x0 = (int)ox * p.stride - p.pad;
     } else if (MODE == MODE_DGRAD) {
-      a_y[i] = (int)oy + p.pad;
-      a_x[i] = (int)ox + p.pad;
+      y0 = (int)oy + p.pad;
+      x0 = (int)ox + p.pad;
     } else {
-      a_y[i] = (int)oy + p.cls_c0y[cls];
-      a_x[i] = (int)ox + p.cls_c0x[cls];
+      y0 = (int)oy + p.cls_c0y[cls];
+      x0 = (int)ox + p.cls_c0x[cls];
     }
+    a_off[i] = (((int)n * p.SH + y0) * p.SW + x0) * p.src_ld + p.src_off;
+    uint32_t msk = 0;
+#pragma unroll
+    for (int t = 0; t < NTAPS; ++t) {
+      int dy, dx;
+      tap_dyx(t, dy, dx);
+      const int iy = y0 + SGN * dy, ix = x0 + SGN * dx;
+      if (row_ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW) msk |= 1u << t;
+    }
+    a_msk[i] = msk;
   }
   int tap = q / p.cpt, cc = q - (q / p.cpt) * p.cpt;
+  constexpr int EPC = 16 / (int)sizeof(T);   // elements per 16-B chunk
 
   u32x4 a_reg[A_SLOTS], b_reg[B_SLOTS];
 
-  auto load_tile = [&](int kt) {
+  // GL: buf = ring stage to fill with LDS-DMA; register path: buf unused (a_reg/b_reg)
+  auto load_tile = [&](int kt, int buf) {
+    char* lds_a = smem + buf * TILE_BYTES + wave * 1024;
+    char* lds_b = smem + buf * TILE_BYTES + BM * PITCH + wave * 1024;
+    (void)lds_a; (void)lds_b;
     const int kc = kt * NT_KCH + q;
-    int kh, kw;
-    if (MODE == MODE_DGRAD2) {
-      kh = ntx == 1 ? tap : (tap >> 1);     // jy
-      kw = ntx == 1 ? 0 : (tap & 1);        // jx
-    } else {
-      kh = tap / KS;
-      kw = tap - (tap / KS) * KS;
-    }
     const bool kok = kc < Kc;
+    int dy, dx;
+    tap_dyx(tap, dy, dx);
+    const int delta = SGN * (dy * p.SW + dx) * p.src_ld + cc * EPC;
+    const uint32_t tbit = 1u << (tap & 31);
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
-      int iy, ix;
-      bool ok = kok && a_ok[i];
-      if (MODE == MODE_FWD) {
-        iy = a_y[i] + kh;
-        ix = a_x[i] + kw;
-      } else if (MODE == MODE_DGRAD2) {
-        iy = a_y[i] - kh;
-        ix = a_x[i] - kw;
-      } else {
-        const int ty = a_y[i] - kh, tx = a_x[i] - kw;
-        if (p.stride == 2) {
-          ok = ok && ((ty | tx) & 1) == 0;
-          iy = ty >> 1;
-          ix = tx >> 1;
-        } else {
-          iy = ty;
-          ix = tx;
-        }
-      }
-      ok = ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW;
-      if (ok) {
-        const long e = ((long)(a_base[i] + iy) * p.SW + ix) * p.src_ld + p.src_off;
-        a_reg[i] = *reinterpret_cast<const u32x4*>(p.src + e * sizeof(T) + cc * 16);
-      } else {
-        a_reg[i] = u32x4{0u, 0u, 0u, 0u};
-      }
+      const bool ok = kok && (a_msk[i] & tbit);
+      const char* ap = ok ? p.src + (long)(a_off[i] + delta) * (long)sizeof(T)
+                          : reinterpret_cast<const char*>(g_zero_chunk);
+      if constexpr (GL) glds16(ap, lds_a + i * 256 * 16);
+      else a_reg[i] = *reinterpret_cast<const u32x4*>(ap);
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
       const int c = tid + 256 * j;
       if (B_CHUNKS >= 256 * (j + 1) || c < B_CHUNKS) {
-        const int row = c / NT_KCH, qq = c % NT_KCH;
+        const int row = c / NT_KCH, qq = GL ? q : c % NT_KCH;   // GL: swizzled source chunk
         const long off = ((long)(n0 + row) * (nkt * NT_KCH) + kt * NT_KCH + qq) * 16;
-        b_reg[j] = *reinterpret_cast<const u32x4*>(wp + off);
+        if constexpr (GL) glds16(wp + off, lds_b + j * 256 * 16);
+        else b_reg[j] = *reinterpret_cast<const u32x4*>(wp + off);
       }
     }
     // advance the tap cursor by one k-tile of chunks
@@ -211,32 +260,38 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
       for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.0f;
 
   const int lr = lane & 31, lh = lane >> 5;
-  // nch: valid 16-B chunks in this k-tile (the tail tile of K may be partial)
-  auto compute = [&](int buf, int nch) {
+  // The whole 128-B k-tile is always computed: chunks beyond K are zero on both sides (A
+  // loads the zero chunk, packed weights are zero-padded), so no branches split the MFMA
+  // stream and the fragment reads of substep s+1 overlap the MFMAs of substep s.
+  auto compute = [&](int buf) {
     const char* A = smem + buf * TILE_BYTES;
-    const char* B = A + BM * NT_ROWP;
+    const char* B = A + BM * PITCH;
     if constexpr (!F32) {
+      u32x4 af[2][TM], bfr[2][TN];
+      const int swz = (lr >> 1) & 7;   // rows of a fragment differ from lr by multiples of 16
+      auto frags = [&](int s, int slot) {
+        const int co = ((2 * s + lh) ^ swz) * 16;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+          af[slot][a] = *reinterpret_cast<const u32x4*>(A + (wm * WTM + a * 32 + lr) * PITCH + co);
+#pragma unroll
+        for (int b = 0; b < TN; ++b)
+          bfr[slot][b] = *reinterpret_cast<const u32x4*>(B + (wn * WTN + b * 32 + lr) * PITCH + co);
+      };
+      frags(0, 0);
 #pragma unroll
       for (int s = 0; s < NT_KCH / 2; ++s) {
-        if (2 * s < nch) {
-          u32x4 af[TM], bfr[TN];
+        if (s + 1 < NT_KCH / 2) frags(s + 1, (s + 1) & 1);
 #pragma unroll
-          for (int a = 0; a < TM; ++a)
-            af[a] = *reinterpret_cast<const u32x4*>(A + (wm * WTM + a * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-          for (int b = 0; b < TN; ++b)
-            bfr[b] = *reinterpret_cast<const u32x4*>(B + (wn * WTN + b * 32 + lr) * NT_ROWP + 32 * s + 16 * lh);
-#pragma unroll
-          for (int a = 0; a < TM; ++a)
-#pragma unroll
-            for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[a], bfr[b], acc[a][b]);
-        }
+          for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[s & 1][a], bfr[s & 1][b], acc[a][b]);
       }
     } else {
       // fp32: per 64-B substep lane (r,h) holds k = 8h..8h+7; MFMA j pairs element j of both halves.
 #pragma unroll
       for (int s = 0; s < NT_KCH / 4; ++s) {
-        if (4 * s < nch) {
+        {
           float af[TM][8], bfr[TN][8];
 #pragma unroll
           for (int a = 0; a < TM; ++a) {
@@ -264,17 +319,42 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
     }
   };
 
-  // ---- main loop: register-staged double buffer, one barrier per 128-B k-tile ----
-  load_tile(0);
-  store_tile(0);
-  __syncthreads();
-  for (int kt = 0; kt < nkt; ++kt) {
-    const int cur = kt & 1;
-    const bool more = kt + 1 < nkt;
-    if (more) load_tile(kt + 1);
-    compute(cur, Kc - kt * NT_KCH);
-    if (more) store_tile(cur ^ 1);
+  if constexpr (GL) {
+    // ---- main loop: ST-deep LDS-DMA ring, one raw barrier per 128-B k-tile ----
+    constexpr int NG = A_SLOTS + B_SLOTS;   // LDS-DMA instructions per thread per k-tile
+#pragma unroll
+    for (int s0 = 0; s0 < ST - 1; ++s0)
+      if (s0 < nkt) load_tile(s0, s0);
+    int stage = 0;
+    for (int kt = 0; kt < nkt; ++kt) {
+      // k-tiles issued after kt (at most ST-2 of them) may stay in flight
+      const int ahead = nkt - 1 - kt;
+      if (ST >= 4 && ahead >= 2) wait_vmcnt<(ST >= 4 ? 2 * NG : 0)>();
+      else if (ST >= 3 && ahead >= 1) wait_vmcnt<(ST >= 3 ? NG : 0)>();
+      else wait_vmcnt<0>();
+      raw_barrier();                        // k-tile kt visible to all; stage of kt-1 free
+      if (kt + ST - 1 < nkt) {
+        int ns = stage + ST - 1;
+        if (ns >= ST) ns -= ST;
+        load_tile(kt + ST - 1, ns);
+      }
+      compute(stage);
+      if (++stage == ST) stage = 0;
+    }
     __syncthreads();
+  } else {
+    // ---- main loop: register-staged double buffer, one barrier per 128-B k-tile ----
+    load_tile(0, 0);
+    store_tile(0);
+    __syncthreads();
+    for (int kt = 0; kt < nkt; ++kt) {
+      const int cur = kt & 1;
+      const bool more = kt + 1 < nkt;
+      if (more) load_tile(kt + 1, 0);
+      compute(cur);
+      if (more) store_tile(cur ^ 1);
+      __syncthreads();
+    }
   }
 
   // ---- epilogue: stage the fp32 tile in LDS, then 16-B coalesced row segments ----
@@ -411,7 +491,8 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int tile_n = blockIdx.x % p.tiles_n, tile_m = blockIdx.x / p.tiles_n;
+  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  const int tile_n = wg % p.tiles_n, tile_m = wg / p.tiles_n;
   const int split = blockIdx.y;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int kt0 = split * p.kt_per_split;
@@ -757,17 +838,20 @@ static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
   if (cfg == 0) {
     p.tiles_n = cdiv(p.Ncols, 128);
     dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
-    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 128, 2, 2>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 128, 2, 2, 2>), grid, dim3(256), 0, st, p);
   } else if (cfg == 1) {
     p.tiles_n = cdiv(p.Ncols, 64);
     dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
-    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 64, 2, 2>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 64, 2, 2, 3>), grid, dim3(256), 0, st, p);
   } else {
     p.tiles_n = cdiv(p.Ncols, 32);
     dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
-    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 32, 4, 1>), grid, dim3(256), 0, st, p);
+    hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3>), grid, dim3(256), 0, st, p);
   }
 }
+
+// the NT loader addresses its source with 32-bit element offsets
+static bool offsets32(long n, long h, long w, long ld) { return n * h * w * ld < (1l << 31) - (1l << 20); }
 
 template <int MODE, int EPI>
 static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hipStream_t st) {
@@ -897,6 +981,7 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   p.stats = stats;
   p.stats_ld = (int)rup(s->cout, 128);
   p.SH = s->h; p.SW = s->w; p.OW = s->wo;
+  if (!offsets32(s->n, s->h, s->w, x_ld)) return YMS_ERR_UNSUPPORTED;
   p.stride = s->stride; p.pad = s->pad;
   p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
   p.M = s->n * s->ho * s->wo;
@@ -921,6 +1006,7 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
   p.dst = (char*)dx;
   p.src_ld = dz_ld; p.src_off = dz_off; p.dst_ld = dx_ld; p.dst_off = dx_off;
   p.SH = s->ho; p.SW = s->wo; p.OW = s->w;
+  if (!offsets32(s->n, s->ho, s->wo, dz_ld)) return YMS_ERR_UNSUPPORTED;
   p.stride = s->stride; p.pad = s->pad;
   p.Ncols = s->cin;
   p.OH = s->h; p.OWx = s->w;

@@ -25,8 +25,15 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));   // 16-B regist
 template <typename T> __device__ __forceinline__ float to_f(T v) { return (float)v; }
 template <typename T> __device__ __forceinline__ T from_f(float v) { return (T)v; }
 
-__device__ __forceinline__ float silu_f(float a) { return a / (1.0f + __expf(-a)); }
-__device__ __forceinline__ float sigmoid_f(float a) { return 1.0f / (1.0f + __expf(-a)); }
+// SiLU / sigmoid with the hardware reciprocal (v_rcp_f32, 1 ulp) instead of an IEEE divide
+// (~10 VALU ops): these run in every conv epilogue and BN kernel.
+__device__ __forceinline__ float sigmoid_f(float a) { return __builtin_amdgcn_rcpf(1.0f + __expf(-a)); }
+__device__ __forceinline__ float silu_f(float a) { return a * sigmoid_f(a); }
+// SiLU'(a) = s (1 + a (1 - s)), s = sigmoid(a); hardware reciprocal (1 ulp) -- gradients only
+__device__ __forceinline__ float dsilu_f(float a) {
+  const float s = __builtin_amdgcn_rcpf(1.0f + __expf(-a));
+  return s * (1.0f + a * (1.0f - s));
+}
 
 // 8 consecutive channel values as floats (16-bit types: one 16-B load; fp32: two).
 template <typename T> struct Vec8;
@@ -78,6 +85,30 @@ __device__ __forceinline__ void store8(T* p, int valid, const float (&v)[8]) {
     for (int i = 0; i < 8; ++i)
       if (i < valid) p[i] = (T)v[i];
   }
+}
+
+// 8 channel values kept in their storage format (4 VGPRs for 16-bit types, 8 for fp32) so
+// that several pixels' loads can be in flight per thread without spending 8 VGPRs each.
+template <typename T> struct Raw8 { u32x4 v[sizeof(T) / 2]; };
+
+template <typename T>
+__device__ __forceinline__ void load_raw8(const T* p, int valid, Raw8<T>& r) {
+  if (valid >= 8) {
+#pragma unroll
+    for (int k = 0; k < (int)(sizeof(T) / 2); ++k) r.v[k] = reinterpret_cast<const u32x4*>(p)[k];
+  } else {
+    T t[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) t[i] = (i < valid) ? p[i] : (T)0.0f;
+    __builtin_memcpy(&r, t, sizeof(t));
+  }
+}
+template <typename T>
+__device__ __forceinline__ void unpack8(const Raw8<T>& r, float (&f)[8]) {
+  T t[8];
+  __builtin_memcpy(t, &r, sizeof(t));
+#pragma unroll
+  for (int i = 0; i < 8; ++i) f[i] = (float)t[i];
 }
 
 // Unsigned 31-bit fast division by a runtime constant (Granlund-Montgomery).
