@@ -456,6 +456,316 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
 }
 
 // ------------------------------------------------------------------------------------------
+// Persistent NT kernel (16-bit types).  Each block walks output tiles lb, lb+G, lb+2G, ...
+// (lb = XCD-remapped block id, G = grid size) as ONE flattened (tile, k-tile) stream: the
+// ST-deep LDS-DMA ring keeps prefetching across tile boundaries, so a tile's epilogue overlaps
+// the next tile's loads and no pipeline fill/drain is paid per tile.  The epilogue applies
+// the affine/SiLU to the fp32 accumulators in registers (BN statistics are reduced from them
+// by cross-lane adds), stages the tile as T through the ring stage just consumed, and writes
+// 16-B row segments (+ residual / + accumulate in fp32).
+// ------------------------------------------------------------------------------------------
+constexpr int NTP_MAX_AFFINE_COLS = 512;   // wider affine outputs use conv_nt_kernel
+
+template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST>
+__global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
+  constexpr int WTM = BM / WGM, WTN = BN / WGN;
+  constexpr int TM = WTM / 32, TN = WTN / 32;
+  constexpr int A_SLOTS = BM / 32;
+  constexpr int B_SLOTS = BN * NT_KCH / 256;
+  constexpr int STAGE = (BM + BN) * 128;
+  constexpr int RED = (EPI == EPI_STATS) ? WGM * 2 * BN * 4 : 0;
+  constexpr int PRM = (EPI == EPI_AFFINE) ? 2 * NTP_MAX_AFFINE_COLS * 4 : 0;
+  static_assert(BN * NT_KCH % 256 == 0 && BM % 32 == 0, "tile");
+  static_assert(BM * BN * (int)sizeof(T) <= STAGE, "staging must fit one ring stage");
+  __shared__ __attribute__((aligned(16))) char smem[ST * STAGE + RED + PRM + 16];
+  float* red = reinterpret_cast<float*>(smem + ST * STAGE);
+  float* prm = reinterpret_cast<float*>(smem + ST * STAGE + RED);   // [scale | shift] per column
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WGN, wn = wave % WGN;
+  const int lr = lane & 31, lh = lane >> 5;
+  int M = p.M, nkt = p.nkt, Kc = p.Kc, ntx = 1, cls = 0;
+  const char* wp = p.wp;
+  FastDiv dv_w = p.div_ow, dv_hw = p.div_ohw;
+  if (MODE == MODE_DGRAD2) {
+    cls = blockIdx.y;
+    M = p.cls_M[cls];
+    nkt = p.cls_nkt[cls];
+    Kc = p.cls_Kc[cls];
+    ntx = p.cls_ntx[cls];
+    wp = p.wp + p.cls_woff[cls];
+    dv_w = p.cls_div_w[cls];
+    dv_hw = p.cls_div_hw[cls];
+  }
+  const int G = gridDim.x;
+  const int lb = xcd_remap(blockIdx.x, G);
+  const int ntiles = ((M + BM - 1) / BM) * p.tiles_n;
+  if (lb >= ntiles || nkt <= 0) return;
+  const int my_tiles = (ntiles - lb + G - 1) / G;
+  const int total = my_tiles * nkt;
+  if constexpr (EPI == EPI_AFFINE) {
+    // per-column BN scale/shift kept in LDS: an epilogue global load would make the compiler
+    // drain (vmcnt(0)) the LDS-DMA prefetch of the next tile
+    for (int c = tid; c < p.Ncols; c += 256) {
+      prm[c] = p.scale ? p.scale[c] : 1.0f;
+      prm[NTP_MAX_AFFINE_COLS + c] = p.shift ? p.shift[c] : 0.0f;
+    }
+    __syncthreads();
+  }
+
+  // ---- loader (runs ST-1 steps ahead of compute) ----
+  constexpr int NTAPS = MODE == MODE_DGRAD2 ? 4 : KS * KS;
+  constexpr int SGN = MODE == MODE_FWD ? 1 : -1;
+  constexpr int EPC = 16 / (int)sizeof(T);
+  auto tap_dyx = [&](int t, int& dy, int& dx) {
+    if (MODE == MODE_DGRAD2) {
+      dy = ntx == 1 ? t : (t >> 1);
+      dx = ntx == 1 ? 0 : (t & 1);
+    } else {
+      dy = t / KS;
+      dx = t - (t / KS) * KS;
+    }
+  };
+  const int q = (tid & 7) ^ ((tid >> 4) & 7), r0 = tid >> 3;   // swizzled source chunk, first row
+  int a_off[A_SLOTS];
+  uint32_t a_msk[A_SLOTS];
+  int tap = 0, cc = 0, ld_kt = 0, ld_tile = lb, ld_n0 = 0;
+  auto setup_rows = [&](int t) {
+    const int m0 = (t / p.tiles_n) * BM;
+    ld_n0 = (t % p.tiles_n) * BN;
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i) {
+      const int m = m0 + r0 + 32 * i;
+      const bool row_ok = m < M;
+      const uint32_t mm = row_ok ? (uint32_t)m : 0u;
+      const uint32_t n = fdiv(mm, dv_hw);
+      const uint32_t rem = mm - n * dv_hw.d;
+      const uint32_t oy = fdiv(rem, dv_w);
+      const uint32_t ox = rem - oy * dv_w.d;
+      int y0, x0;
+      if (MODE == MODE_FWD) {
+        y0 = (int)oy * p.stride - p.pad;
+        x0 = (int)ox * p.stride - p.pad;
+      } else if (MODE == MODE_DGRAD) {
+        y0 = (int)oy + p.pad;
+        x0 = (int)ox + p.pad;
+      } else {
+        y0 = (int)oy + p.cls_c0y[cls];
+        x0 = (int)ox + p.cls_c0x[cls];
+      }
+      a_off[i] = (((int)n * p.SH + y0) * p.SW + x0) * p.src_ld + p.src_off;
+      uint32_t msk = 0;
+#pragma unroll
+      for (int tt = 0; tt < NTAPS; ++tt) {
+        int dy, dx;
+        tap_dyx(tt, dy, dx);
+        const int iy = y0 + SGN * dy, ix = x0 + SGN * dx;
+        if (row_ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW) msk |= 1u << tt;
+      }
+      a_msk[i] = msk;
+    }
+    tap = q / p.cpt;
+    cc = q - tap * p.cpt;
+  };
+  setup_rows(ld_tile);
+  auto issue = [&](int stage) {
+    char* lds_a = smem + stage * STAGE + wave * 1024;
+    char* lds_b = smem + stage * STAGE + BM * 128 + wave * 1024;
+    const int kc = ld_kt * NT_KCH + q;
+    const bool kok = kc < Kc;
+    int dy, dx;
+    tap_dyx(tap, dy, dx);
+    const int delta = SGN * (dy * p.SW + dx) * p.src_ld + cc * EPC;
+    const uint32_t tbit = 1u << (tap & 31);
+#pragma unroll
+    for (int i = 0; i < A_SLOTS; ++i) {
+      const bool ok = kok && (a_msk[i] & tbit);
+      const char* ap = ok ? p.src + (long)(a_off[i] + delta) * (long)sizeof(T)
+                          : reinterpret_cast<const char*>(g_zero_chunk);
+      glds16(ap, lds_a + i * 4096);
+    }
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j) {
+      const int row = j * 32 + r0;
+      const long off = ((long)(ld_n0 + row) * (nkt * NT_KCH) + ld_kt * NT_KCH + q) * 16;
+      glds16(wp + off, lds_b + j * 4096);
+    }
+    cc += NT_KCH;
+    while (cc >= p.cpt) { cc -= p.cpt; ++tap; }
+    if (++ld_kt == nkt) {           // next tile of this block
+      ld_kt = 0;
+      ld_tile += G;
+      if (ld_tile < ntiles) setup_rows(ld_tile);
+    }
+  };
+
+  // ---- compute ----
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int b = 0; b < TN; ++b)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[a][b][i] = 0.0f;
+  const int swz = (lr >> 1) & 7;
+  auto compute = [&](int stage) {
+    const char* A = smem + stage * STAGE;
+    const char* B = A + BM * 128;
+    u32x4 af[2][TM], bfr[2][TN];
+    auto frags = [&](int s, int slot) {
+      const int co = ((2 * s + lh) ^ swz) * 16;
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+        af[slot][a] = *reinterpret_cast<const u32x4*>(A + (wm * WTM + a * 32 + lr) * 128 + co);
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+        bfr[slot][b] = *reinterpret_cast<const u32x4*>(B + (wn * WTN + b * 32 + lr) * 128 + co);
+    };
+    frags(0, 0);
+#pragma unroll
+    for (int s = 0; s < NT_KCH / 2; ++s) {
+      if (s + 1 < NT_KCH / 2) frags(s + 1, (s + 1) & 1);
+#pragma unroll
+      for (int a = 0; a < TM; ++a)
+#pragma unroll
+        for (int b = 0; b < TN; ++b) acc[a][b] = Mfma<T>::mma(af[s & 1][a], bfr[s & 1][b], acc[a][b]);
+    }
+  };
+
+  // ---- epilogue of one tile (staging through ring stage `stage`) ----
+  auto lds_barrier = [&]() {
+    __builtin_amdgcn_s_waitcnt((0xF) | (3 << 14) | (0x7 << 4) | (0 << 8));   // lgkmcnt(0) only
+    raw_barrier();
+  };
+  auto epilogue = [&](int t, int stage) {
+    const int tile_m = t / p.tiles_n, m0 = tile_m * BM, n0 = (t % p.tiles_n) * BN;
+    T* stg = reinterpret_cast<T*>(smem + stage * STAGE);
+    // per-column parameters / statistics from the fp32 accumulators
+    if constexpr (EPI == EPI_STATS) {
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            const float v = acc[a][b][i];
+            s1 += v;
+            s2 += v * v;
+          }
+        s1 += __shfl_xor(s1, 32);
+        s2 += __shfl_xor(s2, 32);
+        if (lh == 0) {
+          red[(wm * 2 + 0) * BN + wn * WTN + b * 32 + lr] = s1;
+          red[(wm * 2 + 1) * BN + wn * WTN + b * 32 + lr] = s2;
+        }
+      }
+    }
+    if constexpr (EPI == EPI_AFFINE) {
+#pragma unroll
+      for (int b = 0; b < TN; ++b) {
+        const int col = n0 + wn * WTN + b * 32 + lr;
+        const bool cv = col < p.Ncols;
+        const float sc = cv ? prm[col] : 1.0f;
+        const float sh = cv ? prm[NTP_MAX_AFFINE_COLS + col] : 0.0f;
+#pragma unroll
+        for (int a = 0; a < TM; ++a)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) {
+            float v = acc[a][b][i] * sc + sh;
+            if (p.act == YMS_ACT_SILU) v = silu_f(v);
+            acc[a][b][i] = v;
+          }
+      }
+    }
+    lds_barrier();      // every wave has finished reading `stage` as MFMA operands
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int b = 0; b < TN; ++b)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          const int rl = wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+          stg[rl * BN + wn * WTN + b * 32 + lr] = (T)acc[a][b][i];
+          acc[a][b][i] = 0.0f;
+        }
+    lds_barrier();
+    if constexpr (EPI == EPI_STATS) {
+      if (tid < BN) {
+        float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+        for (int w = 0; w < WGM; ++w) {
+          t1 += red[(w * 2 + 0) * BN + tid];
+          t2 += red[(w * 2 + 1) * BN + tid];
+        }
+        float* so = p.stats + (long)tile_m * 2 * p.stats_ld;
+        so[n0 + tid] = t1;
+        so[p.stats_ld + n0 + tid] = t2;
+      }
+    }
+    constexpr int CH = BN / 8;      // 16-B chunks per staged row
+    constexpr int RS = 256 / CH;    // rows per pass
+    const int ch = tid % CH, rr = tid / CH;
+    const int col0 = n0 + ch * 8;
+    const int nv = p.Ncols - col0;
+#pragma unroll
+    for (int j = 0; j < BM / RS; ++j) {
+      const int rl = rr + RS * j;
+      int row = m0 + rl;
+      if (row >= M || nv <= 0) continue;
+      float v[8];
+      unpack8(*reinterpret_cast<const Raw8<T>*>(stg + rl * BN + ch * 8), v);
+      if (MODE == MODE_DGRAD2) {
+        const uint32_t n = fdiv((uint32_t)row, dv_hw);
+        const uint32_t rem = (uint32_t)row - n * dv_hw.d;
+        const uint32_t ya = fdiv(rem, dv_w);
+        const uint32_t xb = rem - ya * dv_w.d;
+        row = ((int)n * p.OH + 2 * (int)ya + (cls >> 1)) * p.OWx + 2 * (int)xb + (cls & 1);
+      }
+      T* dst = reinterpret_cast<T*>(p.dst) + (long)row * p.dst_ld + p.dst_off + col0;
+      if (EPI == EPI_AFFINE && p.res) {
+        float r[8];
+        load8(reinterpret_cast<const T*>(p.res) + (long)row * p.res_ld + p.res_off + col0, nv, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += r[i];
+      } else if (EPI == EPI_ACCUM) {
+        float r[8];
+        load8(dst, nv, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) v[i] += r[i];
+      }
+      store8(dst, nv, v);
+    }
+  };
+
+  // ---- flattened (tile, k-tile) stream ----
+  constexpr int NG = A_SLOTS + B_SLOTS;
+#pragma unroll
+  for (int s0 = 0; s0 < ST - 1; ++s0)
+    if (s0 < total) issue(s0);
+  int stage = 0, ckt = 0, ctile = lb;
+  for (int g = 0; g < total; ++g) {
+    const int ahead = total - 1 - g;
+    if (ST >= 4 && ahead >= 2) wait_vmcnt<(ST >= 4 ? 2 * NG : 0)>();
+    else if (ST >= 3 && ahead >= 1) wait_vmcnt<(ST >= 3 ? NG : 0)>();
+    else wait_vmcnt<0>();
+    raw_barrier();
+    if (g + ST - 1 < total) {
+      int ns = stage + ST - 1;
+      if (ns >= ST) ns -= ST;
+      issue(ns);
+    }
+    compute(stage);
+    if (++ckt == nkt) {
+      epilogue(ctile, stage);
+      ckt = 0;
+      ctile += G;
+    }
+    if (++stage == ST) stage = 0;
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // wgrad: TT GEMM over pixels with ds_read_b64_tr_b16 operands, split-K partial slabs.
 // ------------------------------------------------------------------------------------------
 struct TTParams {
@@ -831,10 +1141,45 @@ static TileChoice choose_tile(int ncols) {
   return TileChoice{0, 128};
 }
 
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
+// persistent grid: at most two resident blocks per CU (the kernels are sized for 2/CU);
+// p.M is the largest parity class for DGRAD2
+template <typename K>
+static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, hipStream_t st) {
+  const long ntiles = (long)cdiv(p.M, bm) * p.tiles_n;
+  const unsigned gx = (unsigned)std::max<long>(1, std::min<long>(ntiles, 2L * cu_count()));
+  hipLaunchKernelGGL(kernel, dim3(gx, gy), dim3(256), 0, st, p);
+}
+
 template <typename T, int KS, int MODE, int EPI>
 static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
   NTParams p = p0;
   const unsigned gy = MODE == MODE_DGRAD2 ? 4u : 1u;
+  if constexpr (sizeof(T) == 2) {
+    if (EPI != EPI_AFFINE || p.Ncols <= NTP_MAX_AFFINE_COLS) {
+    if (cfg == 0) {
+      p.tiles_n = cdiv(p.Ncols, 128);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 2, 2>, p, 128, gy, st);
+    } else if (cfg == 1) {
+      p.tiles_n = cdiv(p.Ncols, 64);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 2, 2, 3>, p, 128, gy, st);
+    } else {
+      p.tiles_n = cdiv(p.Ncols, 32);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3>, p, 128, gy, st);
+    }
+    return;
+    }
+  }
   if (cfg == 0) {
     p.tiles_n = cdiv(p.Ncols, 128);
     dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
