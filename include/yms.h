@@ -65,6 +65,18 @@ size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad);
 yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* packed,
                                 int for_dgrad, void* stream);
 
+/* Batched packing (one launch for all of a plan's packs; training repacks every step).
+ * yms_pack_job_init fills a job on the host (YMS_ERR_UNSUPPORTED for stride-2 dgrad packs,
+ * which keep yms_conv_pack_weight); the job array must be in device memory for the launch. */
+typedef struct {
+  const float* w;
+  void* packed;
+  int cout, cin, ks, rows, kp_elems, c8_in, for_dgrad, dtype;
+} yms_pack_job;
+yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* packed, int for_dgrad,
+                             yms_pack_job* job);
+yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* stream);
+
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------------------- */
 /* Number of fp32 rows of BN partial statistics written by yms_conv_fwd(stats != NULL);
  * the stats workspace is [rows][2][stats_ld] floats, stats_ld = yms_conv_stats_ld(). */

@@ -28,12 +28,13 @@ from collections import defaultdict
 def family(name):
     # conv_nt_kernel<T, KS, MODE, EPI, BM, BN, WGM, WGN>: EPI 0 (affine) / 1 (BN stats) are
     # forward launches, 2 (store) / 3 (accumulate) are dgrad launches
-    m = re.search(r"conv_nt_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
+    m = re.search(r"conv_ntp?_kernelI(DF16b|DF16_|f)Li(\d+)ELi(\d+)ELi(\d+)E", name)
     if m:
         return "conv_fwd" if int(m.group(4)) <= 1 else "conv_dgrad"
-    m = re.search(r"conv_nt_kernel<(.*)>", name)
-    if m:   # demangled (rocprof mangles T/KS oddly): count from the end
-        epi = int(m.group(1).split(",")[-5])
+    m = re.search(r"conv_ntp?_kernel<(.*)>", name)
+    if m:   # demangled (rocprof mangles T/KS oddly): count from the end; ntp has a trailing ST
+        args = m.group(1).split(",")
+        epi = int(args[-6 if "conv_ntp" in name else -5])
         return "conv_fwd" if epi <= 1 else "conv_dgrad"
     if "conv_wgrad_kernel" in name or "wgrad_reduce_kernel" in name:
         return "conv_wgrad"
@@ -46,7 +47,7 @@ def family(name):
 
 def is_call_head(name):
     """Kernels that start one yms_conv_* call (the wgrad reducer does not)."""
-    return "conv_nt_kernel" in name or "conv_wgrad_kernel" in name
+    return "conv_nt_kernel" in name or "conv_ntp_kernel" in name or "conv_wgrad_kernel" in name
 
 
 def stats(path):

@@ -375,44 +375,34 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
 // ------------------------------------------------------------------------------------------
 // SPPF pools: slot k = clipped (4k+1)x(4k+1) window max of slot 0 (== k chained MaxPool5).
 // ------------------------------------------------------------------------------------------
+// One MaxPool2d(5, 1, 2) of the SPPF chain: slot `out` = pool5(slot `in`) (-inf padding).
+// The chain p1 = pool(x), p2 = pool(p1), p3 = pool(p2) runs as three launches (75 loads per
+// output group instead of the 169 of a direct 13x13 window); max is exact, so the result is
+// bit-identical to the reference's chained pools.
 template <typename T>
-__global__ void sppf_fwd_kernel(int n, int h, int w, int c, T* buf, int ld, int off) {
-  const int G = (c + 7) >> 3;
-  const long total = (long)n * h * w * G;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
-    const int g = (int)(t % G);
-    long r = t / G;
-    const int x = (int)(r % w);
-    r /= w;
-    const int y = (int)(r % h);
-    const int b = (int)(r / h);
-    const int c0 = g * 8, nv = min(8, c - c0);
-    float m1[8], m2[8], m3[8];
+__global__ __launch_bounds__(256) void pool5_fwd_kernel(int n, int h, int w, int c, T* buf, int ld, int in_off,
+                                                        int out_off) {
+  const int G = c >> 3;
+  const uint32_t total = (uint32_t)n * h * w * G;
+  for (uint32_t t = blockIdx.x * 256u + threadIdx.x; t < total; t += gridDim.x * 256u) {
+    const uint32_t g = t % G, pix = t / G;
+    const uint32_t x = pix % w, r = pix / w;
+    const uint32_t y = r % h, b = r / h;
+    float m[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) { m1[i] = -INFINITY; m2[i] = -INFINITY; m3[i] = -INFINITY; }
-    for (int dy = -6; dy <= 6; ++dy) {
-      const int yy = y + dy;
-      if (yy < 0 || yy >= h) continue;
-      const int ady = dy < 0 ? -dy : dy;
-      for (int dx = -6; dx <= 6; ++dx) {
-        const int xx = x + dx;
-        if (xx < 0 || xx >= w) continue;
-        const int adx = dx < 0 ? -dx : dx;
-        const int rad = ady > adx ? ady : adx;
+    for (int i = 0; i < 8; ++i) m[i] = -INFINITY;
+    const int y0 = max((int)y - 2, 0), y1 = min((int)y + 2, h - 1);
+    const int x0 = max((int)x - 2, 0), x1 = min((int)x + 2, w - 1);
+    for (int yy = y0; yy <= y1; ++yy) {
+      const T* row = buf + ((long)(b * h + yy) * w) * ld + in_off + g * 8;
+      for (int xx = x0; xx <= x1; ++xx) {
         float v[8];
-        load8(buf + (((long)b * h + yy) * w + xx) * ld + off + c0, nv, v);
+        Vec8<T>::load(row + (long)xx * ld, v);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          m3[i] = fmaxf(m3[i], v[i]);
-          if (rad <= 4) m2[i] = fmaxf(m2[i], v[i]);
-          if (rad <= 2) m1[i] = fmaxf(m1[i], v[i]);
-        }
+        for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], v[i]);
       }
     }
-    T* o = buf + (((long)b * h + y) * w + x) * ld + off + c0;
-    store8(o + c, nv, m1);
-    store8(o + 2 * c, nv, m2);
-    store8(o + 3 * c, nv, m3);
+    Vec8<T>::store(buf + (long)pix * ld + out_off + g * 8, m);
   }
 }
 
@@ -421,10 +411,10 @@ template <typename T>
 __global__ void pool5_argmax_kernel(int n, int h, int w, int c, const T* buf, int ld, int in_off,
                                     uint8_t* arg) {
   const int G = (c + 7) >> 3;
-  const long total = (long)n * h * w * G;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const uint32_t total = (uint32_t)n * h * w * G;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int g = (int)(t % G);
-    long r = t / G;
+    uint32_t r = t / G;
     const int x = (int)(r % w);
     r /= w;
     const int y = (int)(r % h);
@@ -461,10 +451,10 @@ template <typename T>
 __global__ void pool5_gather_kernel(int n, int h, int w, int c, const uint8_t* arg, T* g, int ld,
                                     int in_off, int out_off) {
   const int G = (c + 7) >> 3;
-  const long total = (long)n * h * w * G;
-  for (long t = blockIdx.x * (long)blockDim.x + threadIdx.x; t < total; t += (long)gridDim.x * blockDim.x) {
+  const uint32_t total = (uint32_t)n * h * w * G;
+  for (uint32_t t = blockIdx.x * blockDim.x + threadIdx.x; t < total; t += gridDim.x * blockDim.x) {
     const int gg = (int)(t % G);
-    long r = t / G;
+    uint32_t r = t / G;
     const int x = (int)(r % w);
     r /= w;
     const int y = (int)(r % h);
@@ -770,8 +760,11 @@ yms_status yms_sppf_pool_fwd(int dtype, int n, int h, int w, int c, void* buf, i
                              void* stream) {
   if (n <= 0 || h <= 0 || w <= 0 || !buf || !vok(ld, off, 4 * c) || c % 8 != 0) return YMS_ERR_INVALID;
   const long items = (long)n * h * w * ((c + 7) / 8);
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(sppf_fwd_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
-                                               (hipStream_t)stream, n, h, w, c, (T*)buf, ld, off));
+  if (items >= (1l << 31)) return YMS_ERR_UNSUPPORTED;
+  for (int k = 1; k <= 3; ++k)
+    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(pool5_fwd_kernel<T>, dim3(grid_for(items)), dim3(256), 0,
+                                                 (hipStream_t)stream, n, h, w, c, (T*)buf, ld,
+                                                 off + (k - 1) * c, off + k * c));
   return launch_status();
 }
 
@@ -781,6 +774,7 @@ yms_status yms_sppf_pool_bwd(int dtype, int n, int h, int w, int c, const void* 
     return YMS_ERR_INVALID;
   if (ld != gld) return YMS_ERR_UNSUPPORTED;
   const long items = (long)n * h * w * ((c + 7) / 8);
+  if (items >= (1l << 31)) return YMS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
   for (int k = 3; k >= 1; --k) {
     // pool k reads slot k-1 (value buf) and produced slot k; push grad of slot k into slot k-1

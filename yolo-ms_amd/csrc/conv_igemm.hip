@@ -1038,6 +1038,28 @@ __global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, in
   }
 }
 
+// All of a plan's weight packs in one launch (training repacks every step): block (x, job)
+// handles rows x, x + gridDim.x, ... of job `job`; 32-bit index math only.
+__global__ __launch_bounds__(256) void pack_weight_batched_kernel(const yms_pack_job* jobs) {
+  const yms_pack_job j = jobs[blockIdx.y];
+  const int kk = j.ks * j.ks;
+  for (int r = blockIdx.x; r < j.rows; r += gridDim.x) {
+    for (int k = threadIdx.x; k < j.kp_elems; k += 256) {
+      const int tap = k / j.c8_in, c = k - tap * j.c8_in;
+      float v = 0.f;
+      if (tap < kk) {
+        const int co = j.for_dgrad ? c : r;
+        const int ci = j.for_dgrad ? r : c;
+        if (co < j.cout && ci < j.cin) v = j.w[((long)co * j.cin + ci) * kk + tap];
+      }
+      const long o = (long)r * j.kp_elems + k;
+      if (j.dtype == YMS_BF16) reinterpret_cast<bf16*>(j.packed)[o] = (bf16)v;
+      else if (j.dtype == YMS_F16) reinterpret_cast<f16*>(j.packed)[o] = (f16)v;
+      else reinterpret_cast<float*>(j.packed)[o] = v;
+    }
+  }
+}
+
 // stride-2 dgrad: 4 parity-class blocks, block c = [cin_pad128][kp_c]; K = (jy, jx, co8)
 struct Dg2Pack {
   long off[4];       // element offset of each class block
@@ -1258,6 +1280,33 @@ size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad) {
   if (for_dgrad && s->stride == 2) return (size_t)dg2_geo(s).off_elems[4];
   PackGeo g = pack_geo(s, for_dgrad);
   return (size_t)g.rows * g.kp_elems;
+}
+
+yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* packed, int for_dgrad,
+                             yms_pack_job* job) {
+  if (!shape_ok(s) || !w || !packed || !job) return YMS_ERR_INVALID;
+  if (for_dgrad && s->stride == 2) return YMS_ERR_UNSUPPORTED;   // parity-class packing: yms_conv_pack_weight
+  PackGeo g = pack_geo(s, for_dgrad);
+  job->w = w;
+  job->packed = packed;
+  job->cout = s->cout;
+  job->cin = s->cin;
+  job->ks = s->k;
+  job->rows = g.rows;
+  job->kp_elems = g.kp_elems;
+  job->c8_in = g.c8_in;
+  job->for_dgrad = for_dgrad;
+  job->dtype = s->dtype;
+  return YMS_OK;
+}
+
+yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* stream) {
+  if (njobs < 0 || (njobs > 0 && !jobs_dev)) return YMS_ERR_INVALID;
+  if (njobs == 0) return YMS_OK;
+  if (njobs > 65535) return YMS_ERR_UNSUPPORTED;
+  hipLaunchKernelGGL(pack_weight_batched_kernel, dim3(64, (unsigned)njobs), dim3(256), 0, (hipStream_t)stream,
+                     jobs_dev);
+  return launch_status();
 }
 
 yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* packed,

@@ -171,8 +171,6 @@ struct NmsWs {
   int* cls_cnt;      // [n][nc]
   int* cls_off;      // [n][nc]
   int* big;          // [0] = count, then (b, c) pairs of segments with more than NMS_CAP boxes
-  uint64_t* mask;    // [n][A][ceil(A/64)] suppression bitmask rows of the big segments
-  int words;         // ceil(A/64)
 };
 
 // Per image: class histogram, exclusive scan and scatter of (score, anchor) keys into class
@@ -301,12 +299,9 @@ __global__ __launch_bounds__(256) void nms_class_kernel(int A, int nc, const flo
 // Large segments (> NMS_CAP boxes: nc=1, or one dominant class of a random-init model).
 //  nms_big_sort : one 1024-thread block per segment, bitonic sort (LDS when <= 16K keys),
 //                 sorted boxes + anchor ids to global.
-//  nms_big_mask : GPU-wide; one wave per (segment, 64-row block), lane = row, 64-bit words of
-//                 "IoU(i, j) > thr, j > i".  Disjoint boxes take an early exit (ovr = 0, or
-//                 0/0 = NaN, is never > thr for thr >= 0), the ratio compare uses the float
-//                 threshold exactly equivalent to torchvision's double compare.
-//  nms_big_scan : blocked greedy: for 64-candidate block k all 1024 threads OR word k of the
-//                 rows kept so far, then one wave resolves the block's own 64x64 diagonal.
+//  nms_big_greedy: kept-list greedy suppression (below).  Disjoint boxes take an early exit
+//                 (ovr = 0, or 0/0 = NaN, is never > thr for thr >= 0); the ratio compare uses
+//                 the float threshold exactly equivalent to torchvision's double compare.
 constexpr int NMS_BIG_LDS_KEYS = 16384;
 
 __device__ __forceinline__ bool iou_gt_f(const float4& i, const float4& j, float thr_f, bool full) {
@@ -364,96 +359,80 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
   }
 }
 
-__global__ __launch_bounds__(256) void nms_big_mask_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
-  // 4 waves: rows rb*64 .. +63 (one per lane), words w = rb + wave, rb + wave + 4, ...; the 64
-  // column boxes (and their areas) of a word are staged once in LDS and read as broadcasts.
-  __shared__ float4 s_box[4][64];
-  __shared__ float s_area[4][64];
-  const int nbig = ws.big[0];
-  const int rb = blockIdx.x, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  for (int it = blockIdx.y; it < nbig; it += gridDim.y) {
-    const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
-    const int n = ws.cls_cnt[(long)b * nc + c];
-    if (rb * 64 >= n) continue;
-    const int off = ws.cls_off[(long)b * nc + c];
-    const float4* boxes = ws.gboxes + (long)b * A + off;
-    uint64_t* mrow = ws.mask + ((long)b * A + off) * ws.words;
-    const int i = rb * 64 + lane;
-    const int W = (n + 63) >> 6;
-    const float4 bi = i < n ? boxes[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-    const float iarea = (bi.z - bi.x) * (bi.w - bi.y);
-    for (int w = rb + wave; w < W; w += 4) {
-      const int jl = (w << 6) + lane;
-      const float4 bj = jl < n ? boxes[jl] : make_float4(0.f, 0.f, 0.f, 0.f);
-      s_box[wave][lane] = bj;
-      s_area[wave][lane] = (bj.z - bj.x) * (bj.w - bj.y);
-      __builtin_amdgcn_wave_barrier();
-      uint64_t bits = 0;
-      const int jmax = min(64, n - (w << 6));
-      const int jmin = (w == rb) ? lane + 1 : 0;      // only j > i inside the diagonal word
-      for (int t = jmin; t < jmax; ++t) {
-        const float4 o = s_box[wave][t];
-        const float xx1 = fmaxf(bi.x, o.x), yy1 = fmaxf(bi.y, o.y);
-        const float xx2 = fminf(bi.z, o.z), yy2 = fminf(bi.w, o.w);
-        if (!full && (xx2 <= xx1 || yy2 <= yy1)) continue;   // disjoint: IoU 0 (or NaN), never > thr
-        const float ww = fmaxf(0.0f, xx2 - xx1), hh = fmaxf(0.0f, yy2 - yy1);
-        const float inter = ww * hh;
-        const float ovr = inter / (iarea + s_area[wave][t] - inter);
-        if (ovr > thr_f) bits |= 1ull << t;
-      }
-      if (i < n) mrow[(long)i * ws.words + w] = bits;
-      __builtin_amdgcn_wave_barrier();
-    }
-  }
-}
+// Greedy suppression over a sorted big segment, one 1024-thread block per segment: candidates
+// are taken in 64-blocks; all 16 waves test the block against the boxes kept so far (kept list
+// compacted to the front of the segment's sorted box array, read through L1/L2), then wave 0
+// resolves the block itself in score order, visiting only the still-alive candidates.  Work
+// is O(candidates x kept): a random-init model's near-identical boxes keep a few hundred of
+// 6400 candidates, where an all-pairs bitmask would cost 20M IoUs per segment.
+constexpr int NMS_KEPT_LDS = 6144;   // kept boxes mirrored in LDS (96 KB dynamic); beyond: global
 
-__global__ __launch_bounds__(1024) void nms_big_scan_kernel(int A, int nc, NmsWs ws) {
-  __shared__ unsigned long long s_or[16];
-  __shared__ int s_kept;
+__global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
+  extern __shared__ float4 s_kept[];   // [NMS_KEPT_LDS]
+  __shared__ unsigned long long s_sup[16];
+  __shared__ int s_nk;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbig = ws.big[0];
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
     const int n = ws.cls_cnt[(long)b * nc + c];
     const int off = ws.cls_off[(long)b * nc + c];
-    const uint64_t* mrow = ws.mask + ((long)b * A + off) * ws.words;
-    int* idx = ws.scratch + (long)b * A + off;     // sorted anchor ids (input)
-    int* kept_pos = reinterpret_cast<int*>(ws.gboxes + (long)b * A + off);   // sorted positions kept
-    if (tid == 0) s_kept = 0;
+    float4* boxes = ws.gboxes + (long)b * A + off;
+    int* idx = ws.scratch + (long)b * A + off;
+    if (tid == 0) s_nk = 0;
     __syncthreads();
-    const int W = (n + 63) >> 6;
-    for (int k = 0; k < W; ++k) {
-      const int nk = s_kept;
-      unsigned long long acc = 0;
-      for (int r = tid; r < nk; r += 1024) acc |= mrow[(long)kept_pos[r] * ws.words + k];
-#pragma unroll
-      for (int o = 32; o > 0; o >>= 1) acc |= __shfl_xor(acc, o);
-      if (lane == 0) s_or[wave] = acc;
+    for (int blk = 0; blk < n; blk += 64) {
+      const int m = min(64, n - blk);
+      const bool has = lane < m;
+      const float4 cb = has ? boxes[blk + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+      const int cid = has ? idx[blk + lane] : 0;
+      const int nk = s_nk;
+      bool sup = false;
+      if (has) {
+        const int nl = min(nk, NMS_KEPT_LDS);
+        int k = wave;
+        for (; k + 48 < nl; k += 64) {        // 4 independent LDS reads in flight
+          const float4 k0 = s_kept[k], k1 = s_kept[k + 16], k2 = s_kept[k + 32], k3 = s_kept[k + 48];
+          if (iou_gt_f(k0, cb, thr_f, full) || iou_gt_f(k1, cb, thr_f, full) ||
+              iou_gt_f(k2, cb, thr_f, full) || iou_gt_f(k3, cb, thr_f, full)) { sup = true; break; }
+        }
+        if (!sup)
+          for (; k < nk; k += 16)
+            if (iou_gt_f(k < NMS_KEPT_LDS ? s_kept[k] : boxes[k], cb, thr_f, full)) { sup = true; break; }
+      }
+      const unsigned long long sm = __ballot(sup);
+      if (lane == 0) s_sup[wave] = sm;
       __syncthreads();
       if (wave == 0) {
-        unsigned long long sup = 0;
+        unsigned long long allsup = 0;
 #pragma unroll
-        for (int q = 0; q < 16; ++q) sup |= s_or[q];
-        const int i = (k << 6) + lane;
-        const uint64_t diag = i < n ? mrow[(long)i * ws.words + k] : 0ull;
-        const int m = min(64, n - (k << 6));
-        unsigned long long alive = (m == 64 ? ~0ull : ((1ull << m) - 1ull)) & ~sup;
-        for (int t = 0; t < m; ++t) {
-          if ((alive >> t) & 1ull) alive &= ~__shfl(diag, t);
+        for (int q = 0; q < 16; ++q) allsup |= s_sup[q];
+        bool alive = has && !((allsup >> lane) & 1ull);
+        unsigned long long am = __ballot(alive), done = 0;
+        for (;;) {
+          const unsigned long long rem = am & ~done;
+          if (!rem) break;
+          const int i = __builtin_ctzll(rem);     // wave-uniform
+          done |= 1ull << i;
+          float4 bi;                              // v_readlane (SGPR broadcast, no LDS round trip)
+          bi.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.x), i));
+          bi.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.y), i));
+          bi.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.z), i));
+          bi.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.w), i));
+          if (alive && lane > i && iou_gt_f(bi, cb, thr_f, full)) alive = false;
+          am = __ballot(alive);
         }
-        const int pos = nk + __popcll(alive & ((1ull << lane) - 1ull));
-        if ((alive >> lane) & 1ull) kept_pos[pos] = i;
-        if (lane == 0) s_kept = nk + __popcll(alive);
+        const int pos = nk + __popcll(am & ((1ull << lane) - 1ull));
+        if (alive) {          // pos <= blk + lane: only already-consumed slots are overwritten
+          boxes[pos] = cb;
+          idx[pos] = cid;
+          if (pos < NMS_KEPT_LDS) s_kept[pos] = cb;
+        }
+        if (lane == 0) s_nk = nk + __popcll(am);
       }
       __syncthreads();
     }
-    // kept sorted positions -> anchor ids, in score order (positions are increasing)
-    const int nk = s_kept;
-    for (int r = tid; r < nk; r += 1024) kept_pos[r] = idx[kept_pos[r]];   // own element only
-    __syncthreads();
-    for (int r = tid; r < nk; r += 1024) idx[r] = kept_pos[r];
-    __syncthreads();
-    if (tid == 0) ws.cls_cnt[(long)b * nc + c] = nk;
+    if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
     __syncthreads();
   }
 }
@@ -489,9 +468,6 @@ static NmsWs carve(void* ws, int n, int A, int nc) {
   w.cls_off = (int*)p;
   p += r256((size_t)n * nc * 4);
   w.big = (int*)p;
-  p += r256((size_t)(1 + 2 * n * nc) * 4);
-  w.words = (A + 63) / 64;
-  w.mask = (uint64_t*)p;
   return w;
 }
 
@@ -555,8 +531,7 @@ yms_status yms_nms_prep(int n, int A, int nc, const float* pred, float conf, flo
 
 size_t yms_nms_ws_bytes(int n, int A, int nc) {
   return r256((size_t)n * A * 8) + r256((size_t)n * A * 16) + r256((size_t)n * A * 4) +
-         r256((size_t)n * nc * 4) + r256((size_t)n * nc * 4) + r256((size_t)(1 + 2 * n * nc) * 4) +
-         (size_t)n * A * ((A + 63) / 64) * 8;
+         r256((size_t)n * nc * 4) + r256((size_t)n * nc * 4) + r256((size_t)(1 + 2 * n * nc) * 4);
 }
 
 yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, const float* score,
@@ -573,7 +548,9 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)nms_big_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            NMS_BIG_LDS_KEYS * 8) != hipSuccess)
+                            NMS_BIG_LDS_KEYS * 8) != hipSuccess ||
+        hipFuncSetAttribute((const void*)nms_big_greedy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NMS_KEPT_LDS * 16) != hipSuccess)
       return YMS_ERR_LAUNCH;
     attr_set = true;
   }
@@ -585,9 +562,8 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     const unsigned segs = (unsigned)std::min(256, n * nc);
     hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_BIG_LDS_KEYS * 8, st, A, nc,
                        boxes_xyxy, w);
-    hipLaunchKernelGGL(nms_big_mask_kernel, dim3((unsigned)((A + 63) / 64), std::min(64u, segs)), dim3(256), 0, st,
-                       A, nc, thr_f, full, w);
-    hipLaunchKernelGGL(nms_big_scan_kernel, dim3(segs), dim3(1024), 0, st, A, nc, w);
+    hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), (size_t)NMS_KEPT_LDS * 16, st, A, nc,
+                       thr_f, full, w);
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;

@@ -33,6 +33,11 @@ class ConvShape(ctypes.Structure):
                 ("n", "h", "w", "cin", "cout", "k", "stride", "pad", "ho", "wo", "dtype")]
 
 
+class PackJob(ctypes.Structure):
+    _fields_ = [("w", ctypes.c_void_p), ("packed", ctypes.c_void_p)] + [
+        (k, ctypes.c_int) for k in ("cout", "cin", "ks", "rows", "kp_elems", "c8_in", "for_dgrad", "dtype")]
+
+
 _P = ctypes.c_void_p
 _I = ctypes.c_int
 _L = ctypes.c_long
@@ -46,6 +51,8 @@ _SIGS = {
     "yms_status_string": (ctypes.c_char_p, [_I]),
     "yms_conv_packed_elems": (_SZ, [_SP, _I]),
     "yms_conv_pack_weight": (_I, [_SP, _P, _P, _I, _P]),
+    "yms_pack_job_init": (_I, [_SP, _P, _P, _I, ctypes.POINTER(PackJob)]),
+    "yms_conv_pack_weights_batched": (_I, [_I, _P, _P]),
     "yms_conv_stats_rows": (_I, [_SP]),
     "yms_conv_stats_ld": (_I, [_SP]),
     "yms_conv_fwd": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _P]),

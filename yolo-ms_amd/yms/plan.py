@@ -146,6 +146,7 @@ class Rt:
         self.training = training
         self.pg_base = None      # flat fp32 param-grad arena pointer
         self.eval_base = None    # eval cache base pointer (packed weights + folded BN)
+        self.prepacked = False   # training: all weight packs already issued (Plan.prepack)
 
     def a(self, v):
         return self.base + v.buf.off
@@ -200,6 +201,10 @@ class ConvOp:
             plan.need_scratch("coef", 8 * c)
             plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
 
+    def pack_specs(self, base):
+        w = self.mod.conv.weight.data_ptr()
+        return [(self.sp, w, base + self.t_wp, 0), (self.sp, w, base + self.t_wpt, 1)]
+
     def prepare_eval(self, rt):
         m = self.mod
         L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), rt.eval_base + self.e_wp, 0, rt.st)
@@ -220,8 +225,9 @@ class ConvOp:
             return
         m = self.mod
         base = rt.base
-        L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wp, 0, rt.st)
-        L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wpt, 1, rt.st)
+        if not rt.prepacked:
+            L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wp, 0, rt.st)
+            L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wpt, 1, rt.st)
         stats = base + rt.plan.scratch["stats"]
         L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
                None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
@@ -297,12 +303,17 @@ class BiasConvOp:
     def prepare_eval(self, rt):
         L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), rt.eval_base + self.e_wp, 0, rt.st)
 
+    def pack_specs(self, base):
+        w = self.conv.weight.data_ptr()
+        return [(self.sp, w, base + self.t_wp, 0), (self.sp, w, base + self.t_wpt, 1)]
+
     def fwd(self, rt):
         x, y = self.x, self.y
         if rt.training:
             wp = rt.base + self.t_wp
-            L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), wp, 0, rt.st)
-            L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), rt.base + self.t_wpt, 1, rt.st)
+            if not rt.prepacked:
+                L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), wp, 0, rt.st)
+                L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), rt.base + self.t_wpt, 1, rt.st)
         else:
             wp = rt.eval_base + self.e_wp
         L.call("yms_conv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, wp, rt.a(y), y.buf.ld, y.off,
@@ -513,6 +524,35 @@ class Plan:
                     op.prepare_eval(rt)
             self._eval_sig = sig
         return self._eval_arena.data_ptr()
+
+    def prepack(self, rt):
+        """Training: issue every conv weight pack of the step -- one batched launch for the
+        plain packs (device job table cached per arena base) plus the stride-2 dgrad parity
+        packs individually."""
+        specs = [sp for op in self.ops if hasattr(op, "pack_specs") for sp in op.pack_specs(rt.base)]
+        key = tuple((w, dst) for _, w, dst, _ in specs)
+        cache = self.__dict__.setdefault("_pack_tables", {})
+        ent = cache.get(key)
+        if ent is None:
+            jobs, singles = [], []
+            for sp, w, dst, fd in specs:
+                j = L.PackJob()
+                st = L.lib().yms_pack_job_init(sp, w, dst, fd, ctypes.byref(j))
+                if st == 0:
+                    jobs.append(j)
+                else:
+                    singles.append((sp, w, dst, fd))
+            arr = (L.PackJob * max(len(jobs), 1))(*jobs)
+            host = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8)
+            table = host.to(torch.device("cuda", torch.cuda.current_device()))
+            if len(cache) >= 4:
+                cache.clear()
+            ent = cache[key] = (table, len(jobs), singles)
+        table, nj, singles = ent
+        L.call("yms_conv_pack_weights_batched", nj, table.data_ptr(), rt.st)
+        for sp, w, dst, fd in singles:
+            L.call("yms_conv_pack_weight", sp, w, dst, fd, rt.st)
+        rt.prepacked = True
 
     def new_arena(self, device, stream):
         arena = torch.empty(max(self.arena_bytes, 1), dtype=torch.uint8, device=device)

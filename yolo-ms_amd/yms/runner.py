@@ -124,6 +124,7 @@ class _PlanFn(torch.autograd.Function):
         arena = plan.new_arena(dev, stream)
         rt = Rt(plan, arena.data_ptr(), stream, True)
         _load_inputs(plan, rt, inputs)
+        plan.prepack(rt)
         for op in plan.ops:
             op.fwd(rt)
         state.arena = arena
