@@ -42,6 +42,8 @@ struct NTParams {
   int OW;           // row-space width
   int stride, pad;
   int cpt;          // 16-B chunks per tap along source channels
+  uint32_t cpt_magic;   // kc / cpt == (kc * cpt_magic) >> 16 for every kc < nkt * 8 (host-checked)
+  uint32_t src_bytes;   // byte extent of the source view's buffer (raw-buffer num_records, < 2^31)
   int Kc;           // valid K chunks
   int nkt;          // K tiles (4 chunks each)
   int M;            // rows (pixels)
@@ -95,6 +97,14 @@ __device__ __forceinline__ void raw_barrier() {
   asm volatile("" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+}
+// raw-buffer LDS-DMA of 16 B per lane; an offset at or past the resource's num_records loads
+// zeros.  (The builtin is wrapped so the host pass of a kernel template never sees it: clang
+// silently drops the host stub of a template kernel that names it directly.)
+__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (YMS_LDS void*)lds_wave_base, 16, voff, 0, 0, 0);
+#endif
 }
 __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
   __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
@@ -465,8 +475,10 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
 // 16-B row segments (+ residual / + accumulate in fp32).
 // ------------------------------------------------------------------------------------------
 constexpr int NTP_MAX_AFFINE_COLS = 512;   // wider affine outputs use conv_nt_kernel
+constexpr uint32_t NT_OOB = 0x80000000u;    // voffset past every A resource (num_records < 2^31)
+constexpr int NT_RSRC3 = 0x00020000;        // buffer descriptor word 3 (gfx9 raw buffer, 32-bit data)
 
-template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST>
+template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI>
 __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
@@ -514,9 +526,17 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
   }
 
   // ---- loader (runs ST-1 steps ahead of compute) ----
+  // Raw-buffer LDS-DMA (buffer_load_dwordx4 ... lds): a lane whose im2col element lies outside
+  // the image (or past K) gets voffset = NT_OOB, beyond the resource's num_records, and the
+  // hardware writes zeros into its LDS slot -- no exec-masked branches, no 64-bit address
+  // arithmetic.  UNI (cpt % 8 == 0): every lane of a k-tile sits in the same tap, so the tap
+  // offset is scalar and each A slot costs one bit test, one add and one select.
   constexpr int NTAPS = MODE == MODE_DGRAD2 ? 4 : KS * KS;
   constexpr int SGN = MODE == MODE_FWD ? 1 : -1;
-  constexpr int EPC = 16 / (int)sizeof(T);
+  constexpr int ES = (int)sizeof(T);
+  const __amdgpu_buffer_rsrc_t rs_a =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)p.src_bytes, NT_RSRC3);
+  const __amdgpu_buffer_rsrc_t rs_b = __builtin_amdgcn_make_buffer_rsrc((void*)wp, (short)0, 0x7fffffff, NT_RSRC3);
   auto tap_dyx = [&](int t, int& dy, int& dx) {
     if (MODE == MODE_DGRAD2) {
       dy = ntx == 1 ? t : (t >> 1);
@@ -527,12 +547,15 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
     }
   };
   const int q = (tid & 7) ^ ((tid >> 4) & 7), r0 = tid >> 3;   // swizzled source chunk, first row
-  int a_off[A_SLOTS];
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int tap_row = p.SW * p.src_ld * ES;                    // bytes per source image row
+  int a_base[A_SLOTS];                                          // byte offset of tap 0 (+ lane chunk)
   uint32_t a_msk[A_SLOTS];
-  int tap = 0, cc = 0, ld_kt = 0, ld_tile = lb, ld_n0 = 0;
+  uint32_t b_base[B_SLOTS];
+  int tap = 0, cc = 0, ld_kt = 0, ld_tile = lb;
   auto setup_rows = [&](int t) {
     const int m0 = (t / p.tiles_n) * BM;
-    ld_n0 = (t % p.tiles_n) * BN;
+    const int n0 = (t % p.tiles_n) * BN;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
       const int m = m0 + r0 + 32 * i;
@@ -553,7 +576,7 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
         y0 = (int)oy + p.cls_c0y[cls];
         x0 = (int)ox + p.cls_c0x[cls];
       }
-      a_off[i] = (((int)n * p.SH + y0) * p.SW + x0) * p.src_ld + p.src_off;
+      a_base[i] = ((((int)n * p.SH + y0) * p.SW + x0) * p.src_ld + p.src_off) * ES + (UNI ? q * 16 : 0);
       uint32_t msk = 0;
 #pragma unroll
       for (int tt = 0; tt < NTAPS; ++tt) {
@@ -564,34 +587,56 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
       }
       a_msk[i] = msk;
     }
-    tap = q / p.cpt;
-    cc = q - tap * p.cpt;
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j)
+      b_base[j] = (uint32_t)(((n0 + j * 32 + r0) * (nkt * NT_KCH) + q) * 16);
+    tap = 0;
+    cc = 0;
   };
   setup_rows(ld_tile);
   auto issue = [&](int stage) {
-    char* lds_a = smem + stage * STAGE + wave * 1024;
-    char* lds_b = smem + stage * STAGE + BM * 128 + wave * 1024;
-    const int kc = ld_kt * NT_KCH + q;
-    const bool kok = kc < Kc;
-    int dy, dx;
-    tap_dyx(tap, dy, dx);
-    const int delta = SGN * (dy * p.SW + dx) * p.src_ld + cc * EPC;
-    const uint32_t tbit = 1u << (tap & 31);
+    char* lds_a = smem + stage * STAGE + wv * 1024;
+    char* lds_b = smem + stage * STAGE + BM * 128 + wv * 1024;
+    if constexpr (UNI) {
+      // scalar tap / channel position of this k-tile
+      int dy, dx;
+      tap_dyx(tap, dy, dx);
+      const int delta = SGN * (dy * tap_row + dx * p.src_ld * ES) + cc * 16;
 #pragma unroll
-    for (int i = 0; i < A_SLOTS; ++i) {
-      const bool ok = kok && (a_msk[i] & tbit);
-      const char* ap = ok ? p.src + (long)(a_off[i] + delta) * (long)sizeof(T)
-                          : reinterpret_cast<const char*>(g_zero_chunk);
-      glds16(ap, lds_a + i * 4096);
-    }
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const uint32_t vo = ((a_msk[i] >> tap) & 1u) ? (uint32_t)(a_base[i] + delta) : NT_OOB;
+        blds16(rs_a, lds_a + i * 4096, vo);
+      }
+      cc += NT_KCH;
+      if (cc >= p.cpt) { cc = 0; ++tap; }
+    } else {
+      // per-lane K position: kc = kt*8 + q, tap = kc / cpt (exact multiply-shift, host-checked)
+      const int kc = ld_kt * NT_KCH + q;
+      const int lt = (int)(((uint32_t)kc * p.cpt_magic) >> 16);
+      const int lc = kc - lt * p.cpt;
+      int dy, dx;
+      if (MODE == MODE_DGRAD2) {
+        dy = ntx == 1 ? lt : (lt >> 1);
+        dx = ntx == 1 ? 0 : (lt & 1);
+      } else if (KS == 3) {
+        dy = (lt * 11) >> 5;          // lt / 3 for lt < 9
+        dx = lt - 3 * dy;
+      } else {
+        dy = 0;
+        dx = 0;
+      }
+      const int delta = SGN * (dy * tap_row + dx * p.src_ld * ES) + lc * 16;
+      const uint32_t tb = kc < Kc ? (1u << lt) : 0u;
 #pragma unroll
-    for (int j = 0; j < B_SLOTS; ++j) {
-      const int row = j * 32 + r0;
-      const long off = ((long)(ld_n0 + row) * (nkt * NT_KCH) + ld_kt * NT_KCH + q) * 16;
-      glds16(wp + off, lds_b + j * 4096);
+      for (int i = 0; i < A_SLOTS; ++i) {
+        const uint32_t vo = (a_msk[i] & tb) ? (uint32_t)(a_base[i] + delta) : NT_OOB;
+        blds16(rs_a, lds_a + i * 4096, vo);
+      }
     }
-    cc += NT_KCH;
-    while (cc >= p.cpt) { cc -= p.cpt; ++tap; }
+    const int kb = ld_kt * (NT_KCH * 16);
+#pragma unroll
+    for (int j = 0; j < B_SLOTS; ++j)
+      blds16(rs_b, lds_b + j * 4096, b_base[j] + kb);
     if (++ld_kt == nkt) {           // next tile of this block
       ld_kt = 0;
       ld_tile += G;
@@ -1183,23 +1228,30 @@ static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, 
   hipLaunchKernelGGL(kernel, dim3(gx, gy), dim3(256), 0, st, p);
 }
 
+template <typename T, int KS, int MODE, int EPI, bool UNI>
+static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st) {
+  NTParams p = p0;
+  if (cfg == 0) {
+    p.tiles_n = cdiv(p.Ncols, 128);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 2, 2, UNI>, p, 128, gy, st);
+  } else if (cfg == 1) {
+    p.tiles_n = cdiv(p.Ncols, 64);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 2, 2, 3, UNI>, p, 128, gy, st);
+  } else {
+    p.tiles_n = cdiv(p.Ncols, 32);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3, UNI>, p, 128, gy, st);
+  }
+}
+
 template <typename T, int KS, int MODE, int EPI>
 static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
   NTParams p = p0;
   const unsigned gy = MODE == MODE_DGRAD2 ? 4u : 1u;
   if constexpr (sizeof(T) == 2) {
     if (EPI != EPI_AFFINE || p.Ncols <= NTP_MAX_AFFINE_COLS) {
-    if (cfg == 0) {
-      p.tiles_n = cdiv(p.Ncols, 128);
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 2, 2>, p, 128, gy, st);
-    } else if (cfg == 1) {
-      p.tiles_n = cdiv(p.Ncols, 64);
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 2, 2, 3>, p, 128, gy, st);
-    } else {
-      p.tiles_n = cdiv(p.Ncols, 32);
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3>, p, 128, gy, st);
-    }
-    return;
+      if (p.cpt % NT_KCH == 0) launch_ntp<T, KS, MODE, EPI, true>(p, cfg, gy, st);
+      else launch_ntp<T, KS, MODE, EPI, false>(p, cfg, gy, st);
+      return;
     }
   }
   if (cfg == 0) {
@@ -1215,6 +1267,17 @@ static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
     dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
     hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3>), grid, dim3(256), 0, st, p);
   }
+}
+
+// raw-buffer source extent and the exact kc / cpt multiply-shift for the 16-bit loader
+static bool set_src_geometry(NTParams& p, long n, long h, long w, long ld, int es, int max_kc) {
+  const long bytes = n * h * w * ld * es;
+  if (es == 2 && bytes >= (1l << 31) - (1l << 20)) return false;
+  p.src_bytes = (uint32_t)std::min<long>(bytes, 0x7fffffffl);
+  p.cpt_magic = (65536u + (uint32_t)p.cpt - 1) / (uint32_t)p.cpt;
+  for (int kc = 0; kc < max_kc; ++kc)
+    if ((int)(((uint32_t)kc * p.cpt_magic) >> 16) != kc / p.cpt) return false;
+  return true;
 }
 
 // the NT loader addresses its source with 32-bit element offsets
@@ -1378,6 +1441,7 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   if (!offsets32(s->n, s->h, s->w, x_ld)) return YMS_ERR_UNSUPPORTED;
   p.stride = s->stride; p.pad = s->pad;
   p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
+  if (!set_src_geometry(p, s->n, s->h, s->w, x_ld, es, g.nkt * NT_KCH)) return YMS_ERR_UNSUPPORTED;
   p.M = s->n * s->ho * s->wo;
   p.Ncols = s->cout;
   p.div_ow = make_fastdiv(s->wo);
@@ -1410,6 +1474,8 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
     Dg2Geo d = dg2_geo(s);
     const int es = elem_size(s->dtype);
     p.cpt = d.cpt;
+    if (!set_src_geometry(p, s->n, s->ho, s->wo, dz_ld, es, *std::max_element(d.nkt, d.nkt + 4) * NT_KCH))
+      return YMS_ERR_UNSUPPORTED;
     p.M = 0;
     for (int c = 0; c < 4; ++c) {
       p.cls_M[c] = d.M[c];
@@ -1429,6 +1495,8 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
   }
   PackGeo g = pack_geo(s, 1);
   p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
+  if (!set_src_geometry(p, s->n, s->ho, s->wo, dz_ld, elem_size(s->dtype), g.nkt * NT_KCH))
+    return YMS_ERR_UNSUPPORTED;
   p.M = s->n * s->h * s->w;
   p.div_ow = make_fastdiv(s->w);
   p.div_ohw = make_fastdiv(s->h * s->w);
