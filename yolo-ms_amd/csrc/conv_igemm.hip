@@ -90,6 +90,15 @@ template <> struct Mfma<f16> {
 template <int N> __device__ __forceinline__ void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
 }
+// wait until at most min(n, MAXN) k-tiles of NG loads each are still in flight
+template <int NG, int MAXN> __device__ __forceinline__ void wait_tiles(int n) {
+  if constexpr (MAXN > 0) {
+    if (n >= MAXN) { wait_vmcnt<MAXN * NG>(); return; }
+    wait_tiles<NG, MAXN - 1>(n);
+  } else {
+    wait_vmcnt<0>();
+  }
+}
 // workgroup barrier that does NOT drain the vector-memory counter (so LDS-DMA loads of later
 // k-tiles stay in flight across it); the clobbers keep the compiler from moving LDS accesses
 // across it.
@@ -478,16 +487,20 @@ constexpr int NTP_MAX_AFFINE_COLS = 512;   // wider affine outputs use conv_nt_k
 constexpr uint32_t NT_OOB = 0x80000000u;    // voffset past every A resource (num_records < 2^31)
 constexpr int NT_RSRC3 = 0x00020000;        // buffer descriptor word 3 (gfx9 raw buffer, 32-bit data)
 
-template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI>
-__global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
+template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI, int OCC = 2>
+__global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams p) {
+  constexpr int NTHR = WGM * WGN * 64;
+  constexpr int RPP = NTHR / NT_KCH;                       // rows per load pass (one slot)
+  constexpr int SLOT = RPP * 128;                          // LDS bytes per slot
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
-  constexpr int A_SLOTS = BM / 32;
-  constexpr int B_SLOTS = BN * NT_KCH / 256;
+  constexpr int A_SLOTS = BM / RPP;
+  constexpr bool B_PART = BN < RPP;                         // only the first BN/8 waves load B
+  constexpr int B_SLOTS = B_PART ? 1 : BN / RPP;
   constexpr int STAGE = (BM + BN) * 128;
   constexpr int RED = (EPI == EPI_STATS) ? WGM * 2 * BN * 4 : 0;
   constexpr int PRM = (EPI == EPI_AFFINE) ? 2 * NTP_MAX_AFFINE_COLS * 4 : 0;
-  static_assert(BN * NT_KCH % 256 == 0 && BM % 32 == 0, "tile");
+  static_assert((B_PART || BN % RPP == 0) && BM % RPP == 0 && BN <= NTHR, "tile");
   static_assert(BM * BN * (int)sizeof(T) <= STAGE, "staging must fit one ring stage");
   __shared__ __attribute__((aligned(16))) char smem[ST * STAGE + RED + PRM + 16];
   float* red = reinterpret_cast<float*>(smem + ST * STAGE);
@@ -518,7 +531,7 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
   if constexpr (EPI == EPI_AFFINE) {
     // per-column BN scale/shift kept in LDS: an epilogue global load would make the compiler
     // drain (vmcnt(0)) the LDS-DMA prefetch of the next tile
-    for (int c = tid; c < p.Ncols; c += 256) {
+    for (int c = tid; c < p.Ncols; c += NTHR) {
       prm[c] = p.scale ? p.scale[c] : 1.0f;
       prm[NTP_MAX_AFFINE_COLS + c] = p.shift ? p.shift[c] : 0.0f;
     }
@@ -558,7 +571,7 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
     const int n0 = (t % p.tiles_n) * BN;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
-      const int m = m0 + r0 + 32 * i;
+      const int m = m0 + r0 + RPP * i;
       const bool row_ok = m < M;
       const uint32_t mm = row_ok ? (uint32_t)m : 0u;
       const uint32_t n = fdiv(mm, dv_hw);
@@ -589,7 +602,7 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j)
-      b_base[j] = (uint32_t)(((n0 + j * 32 + r0) * (nkt * NT_KCH) + q) * 16);
+      b_base[j] = (uint32_t)(((n0 + j * RPP + r0) * (nkt * NT_KCH) + q) * 16);
     tap = 0;
     cc = 0;
   };
@@ -605,7 +618,7 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         const uint32_t vo = ((a_msk[i] >> tap) & 1u) ? (uint32_t)(a_base[i] + delta) : NT_OOB;
-        blds16(rs_a, lds_a + i * 4096, vo);
+        blds16(rs_a, lds_a + i * SLOT, vo);
       }
       cc += NT_KCH;
       if (cc >= p.cpt) { cc = 0; ++tap; }
@@ -630,13 +643,15 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
 #pragma unroll
       for (int i = 0; i < A_SLOTS; ++i) {
         const uint32_t vo = (a_msk[i] & tb) ? (uint32_t)(a_base[i] + delta) : NT_OOB;
-        blds16(rs_a, lds_a + i * 4096, vo);
+        blds16(rs_a, lds_a + i * SLOT, vo);
       }
     }
     const int kb = ld_kt * (NT_KCH * 16);
+    if (!B_PART || wv * 8 < BN) {
 #pragma unroll
-    for (int j = 0; j < B_SLOTS; ++j)
-      blds16(rs_b, lds_b + j * 4096, b_base[j] + kb);
+      for (int j = 0; j < B_SLOTS; ++j)
+        blds16(rs_b, lds_b + j * SLOT, b_base[j] + kb);
+    }
     if (++ld_kt == nkt) {           // next tile of this block
       ld_kt = 0;
       ld_tile += G;
@@ -749,7 +764,7 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
       }
     }
     constexpr int CH = BN / 8;      // 16-B chunks per staged row
-    constexpr int RS = 256 / CH;    // rows per pass
+    constexpr int RS = NTHR / CH;   // rows per pass
     const int ch = tid % CH, rr = tid / CH;
     const int col0 = n0 + ch * 8;
     const int nv = p.Ncols - col0;
@@ -791,9 +806,10 @@ __global__ __launch_bounds__(256, 2) void conv_ntp_kernel(NTParams p) {
   int stage = 0, ckt = 0, ctile = lb;
   for (int g = 0; g < total; ++g) {
     const int ahead = total - 1 - g;
-    if (ST >= 4 && ahead >= 2) wait_vmcnt<(ST >= 4 ? 2 * NG : 0)>();
-    else if (ST >= 3 && ahead >= 1) wait_vmcnt<(ST >= 3 ? NG : 0)>();
-    else wait_vmcnt<0>();
+    // tile g landed; up to ST-2 later tiles stay in flight (counts are per wave: B_PART waves
+    // past the B rows issue only the A loads)
+    if (!B_PART || wv * 8 < BN) wait_tiles<NG, ST - 2>(ahead);
+    else wait_tiles<A_SLOTS, ST - 2>(ahead);
     raw_barrier();
     if (g + ST - 1 < total) {
       int ns = stage + ST - 1;
@@ -1222,24 +1238,33 @@ static int cu_count() {
 // persistent grid: at most two resident blocks per CU (the kernels are sized for 2/CU);
 // p.M is the largest parity class for DGRAD2
 template <typename K>
-static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, hipStream_t st) {
+static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, hipStream_t st, int occ, int nthr) {
   const long ntiles = (long)cdiv(p.M, bm) * p.tiles_n;
-  const unsigned gx = (unsigned)std::max<long>(1, std::min<long>(ntiles, 2L * cu_count()));
-  hipLaunchKernelGGL(kernel, dim3(gx, gy), dim3(256), 0, st, p);
+  const unsigned gx = (unsigned)std::max<long>(1, std::min<long>(ntiles, (long)occ * cu_count()));
+  hipLaunchKernelGGL(kernel, dim3(gx, gy), dim3(nthr), 0, st, p);
 }
 
 template <typename T, int KS, int MODE, int EPI, bool UNI>
 static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st) {
   NTParams p = p0;
+  static const int variant = getenv("YMS_NT_VARIANT") ? atoi(getenv("YMS_NT_VARIANT")) : 0;
+  // 8-wave blocks at 2-3 blocks per CU: 4-6 waves per SIMD hide the ds_read -> MFMA and barrier
+  // latencies that a 4-wave block at 2/CU exposes (1.6-2x measured on the 3x3 layers).
   if (cfg == 0) {
     p.tiles_n = cdiv(p.Ncols, 128);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 2, 2, UNI>, p, 128, gy, st);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, 2, 512);
   } else if (cfg == 1) {
     p.tiles_n = cdiv(p.Ncols, 64);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 2, 2, 3, UNI>, p, 128, gy, st);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, 3, 512);
+  } else if (MODE == MODE_FWD && variant == 4) {
+    p.tiles_n = cdiv(p.Ncols, 32);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, 2, 512);
+  } else if (MODE == MODE_FWD && variant == 5) {
+    p.tiles_n = cdiv(p.Ncols, 32);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 3, UNI, 2>, p, 256, gy, st, 2, 512);
   } else {
     p.tiles_n = cdiv(p.Ncols, 32);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3, UNI>, p, 128, gy, st);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3, UNI>, p, 128, gy, st, 2, 256);
   }
 }
 
