@@ -839,25 +839,42 @@ struct TTParams {
   int Kc;        // valid kf chunks
   int M;         // pixels (rows of dz)
   int cout8;     // cout rounded up to 8 (valid dz channels incl. zero pad)
-  int nkt;       // pixel tiles of 32
+  int nkt;       // pixel tiles of KP
+  uint32_t dz_bytes, x_bytes;   // raw-buffer extents of dz and x (< 2^31)
   int kt_per_split;
   int tiles_n;   // kf tiles
   int slab_rows, slab_ld;
   FastDiv div_ow, div_ohw;
 };
 
-template <typename T, int KS, int BM, int BN>
-__global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
-  constexpr int WGM = 2, WGN = 2;
+// raw-buffer 16-B load into registers; an offset at or past num_records returns zeros
+// (device-only wrapper, see blds16)
+__device__ __forceinline__ u32x4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t voff) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_bit_cast(u32x4, __builtin_amdgcn_raw_buffer_load_b128(r, voff, 0, 0));
+#else
+  (void)r; (void)voff;
+  return u32x4{0u, 0u, 0u, 0u};
+#endif
+}
+
+// KP pixels per k-tile, NW waves per block, OCC blocks per CU.  Operands are register-staged
+// through raw-buffer loads (out-of-image / out-of-range lanes read zeros: no branches, 32-bit
+// offsets) into padded LDS images consumed by the transposing ds_read_b64_tr_b16.
+template <typename T, int KS, int BM, int BN, int KP, int NW, int OCC>
+__global__ __launch_bounds__(NW * 64, OCC) void conv_wgrad_kernel(TTParams p) {
+  constexpr int NTHR = NW * 64;
+  constexpr int WGN = (NW == 8 && BN >= 128) ? 4 : 2, WGM = NW / WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
+  static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0 && KP % 16 == 0, "wgrad tile");
   constexpr int SZ = sizeof(T);
   constexpr bool F32 = SZ == 4;
   constexpr int EPC = 16 / SZ;                 // elements per chunk
   constexpr int PA = BM * SZ + 64, PB = BN * SZ + 64;   // LDS pitches (conflict-free tr reads)
   constexpr int CA = BM / EPC, CB = BN / EPC;  // chunks per LDS row
-  constexpr int A_SLOTS = (32 * CA + 255) / 256, B_SLOTS = (32 * CB + 255) / 256;
-  constexpr int TILE = 32 * (PA + PB);
+  constexpr int A_SLOTS = (KP * CA + NTHR - 1) / NTHR, B_SLOTS = (KP * CB + NTHR - 1) / NTHR;
+  constexpr int TILE = KP * (PA + PB);
   __shared__ __attribute__((aligned(16))) char smem[2 * TILE];
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -869,16 +886,31 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
   const int kt0 = split * p.kt_per_split;
   const int kt1 = min(p.nkt, kt0 + p.kt_per_split);
 
+  const __amdgpu_buffer_rsrc_t rs_a =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.dz, (short)0, (int)p.dz_bytes, NT_RSRC3);
+  const __amdgpu_buffer_rsrc_t rs_b =
+      __builtin_amdgcn_make_buffer_rsrc((void*)p.x, (short)0, (int)p.x_bytes, NT_RSRC3);
+  const uint32_t dz_row = (uint32_t)(p.dz_ld * SZ);
+  // A-side (dz) slots: fixed pixel row within the k-tile and fixed channel chunk
+  int a_row[A_SLOTS];
+  uint32_t a_col[A_SLOTS];
+#pragma unroll
+  for (int i = 0; i < A_SLOTS; ++i) {
+    const int c = tid + NTHR * i;
+    a_row[i] = c / CA;
+    const int ch = m0 + (c - a_row[i] * CA) * EPC;
+    a_col[i] = (c < KP * CA && ch < p.cout8) ? (uint32_t)((p.dz_off + ch) * SZ) : NT_OOB;
+  }
   // B-side (x im2col) chunk columns are fixed per slot: precompute tap decomposition.
   int b_row[B_SLOTS], b_kh[B_SLOTS], b_kw[B_SLOTS], b_cc[B_SLOTS], b_col[B_SLOTS];
   bool b_kok[B_SLOTS];
 #pragma unroll
   for (int j = 0; j < B_SLOTS; ++j) {
-    const int c = tid + 256 * j;
+    const int c = tid + NTHR * j;
     b_row[j] = c / CB;
     b_col[j] = c - b_row[j] * CB;
     const int kc = n0 / EPC + b_col[j];
-    b_kok[j] = (c < 32 * CB) && kc < p.Kc;
+    b_kok[j] = (c < KP * CB) && kc < p.Kc;
     const int t = kc / p.cpt;
     b_cc[j] = kc - t * p.cpt;
     b_kh[j] = t / KS;
@@ -887,17 +919,12 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
   u32x4 a_reg[A_SLOTS], b_reg[B_SLOTS];
 
   auto load_tile = [&](int kt) {
-    const int q0 = kt * 32;
+    const int q0 = kt * KP;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
-      const int c = tid + 256 * i;
-      const int row = c / CA, col = c - (c / CA) * CA;
-      const int qpix = q0 + row;
-      const int ch = m0 + col * EPC;
-      if (c < 32 * CA && qpix < p.M && ch < p.cout8)
-        a_reg[i] = *reinterpret_cast<const u32x4*>(p.dz + ((long)qpix * p.dz_ld + p.dz_off + ch) * SZ);
-      else
-        a_reg[i] = u32x4{0u, 0u, 0u, 0u};
+      const int qpix = q0 + a_row[i];
+      const bool ok = a_col[i] != NT_OOB && qpix < p.M;
+      a_reg[i] = bld16(rs_a, ok ? (uint32_t)qpix * dz_row + a_col[i] : NT_OOB);
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
@@ -911,26 +938,22 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
       const int iy = (int)oy * p.stride - p.pad + b_kh[j];
       const int ix = (int)ox * p.stride - p.pad + b_kw[j];
       ok = ok && iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW;
-      if (ok) {
-        const long e = (((long)n * p.SH + iy) * p.SW + ix) * p.x_ld + p.x_off;
-        b_reg[j] = *reinterpret_cast<const u32x4*>(p.x + e * SZ + b_cc[j] * 16);
-      } else {
-        b_reg[j] = u32x4{0u, 0u, 0u, 0u};
-      }
+      const uint32_t e = (uint32_t)((((int)n * p.SH + iy) * p.SW + ix) * p.x_ld + p.x_off);
+      b_reg[j] = bld16(rs_b, ok ? e * SZ + (uint32_t)(b_cc[j] * 16) : NT_OOB);
     }
   };
   auto store_tile = [&](int buf) {
     char* A = smem + buf * TILE;
-    char* B = A + 32 * PA;
+    char* B = A + KP * PA;
 #pragma unroll
     for (int i = 0; i < A_SLOTS; ++i) {
-      const int c = tid + 256 * i;
-      if (c < 32 * CA) *reinterpret_cast<u32x4*>(A + (c / CA) * PA + (c % CA) * 16) = a_reg[i];
+      const int c = tid + NTHR * i;
+      if (c < KP * CA) *reinterpret_cast<u32x4*>(A + (c / CA) * PA + (c % CA) * 16) = a_reg[i];
     }
 #pragma unroll
     for (int j = 0; j < B_SLOTS; ++j) {
-      const int c = tid + 256 * j;
-      if (c < 32 * CB) *reinterpret_cast<u32x4*>(B + b_row[j] * PB + b_col[j] * 16) = b_reg[j];
+      const int c = tid + NTHR * j;
+      if (c < KP * CB) *reinterpret_cast<u32x4*>(B + b_row[j] * PB + b_col[j] * 16) = b_reg[j];
     }
   };
 
@@ -949,10 +972,10 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
 
   auto compute = [&](int buf) {
     const char* A = smem + buf * TILE;
-    const char* B = A + 32 * PA;
+    const char* B = A + KP * PA;
     if constexpr (!F32) {
 #pragma unroll
-      for (int s = 0; s < 2; ++s) {
+      for (int s = 0; s < KP / 16; ++s) {
         u32x4 af[TM], bfr[TN];
 #pragma unroll
         for (int a = 0; a < TM; ++a) {
@@ -983,7 +1006,7 @@ __global__ __launch_bounds__(256) void conv_wgrad_kernel(TTParams p) {
       }
     } else {
 #pragma unroll
-      for (int j = 0; j < 16; ++j) {
+      for (int j = 0; j < KP / 2; ++j) {
         float av[TM], bv[TN];
 #pragma unroll
         for (int a = 0; a < TM; ++a)
@@ -1324,8 +1347,14 @@ static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hip
 static int rows_for(int M, int cfg) { (void)cfg; return cdiv(M, 128); }
 
 struct WgradPlan {
-  int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc;
+  int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc, kp, var;
 };
+// wgrad kernel variant for 16-bit types: 0 = 32-pixel k-tiles / 4 waves, 1 = 64 / 4 waves,
+// 2 = 64 / 8 waves (1 block per CU), 3 = 32 / 8 waves.  YMS_WG_VARIANT overrides (dev A/B).
+static int wgrad_variant(int dtype) {
+  static const int v = getenv("YMS_WG_VARIANT") ? atoi(getenv("YMS_WG_VARIANT")) : 0;
+  return dtype == YMS_F32 ? 0 : v;
+}
 static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   WgradPlan w;
   const int es = elem_size(s->dtype);
@@ -1339,22 +1368,42 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   w.tiles_n = cdiv(kf, w.bn);
   w.slab_rows = w.tiles_m * w.bm;
   w.slab_ld = w.tiles_n * w.bn;
+  w.var = wgrad_variant(s->dtype);
+  w.kp = (w.var == 1 || w.var == 2) ? 64 : 32;
   const long M = (long)s->n * s->ho * s->wo;
-  w.nkt = cdiv(M, 32);
+  w.nkt = cdiv(M, w.kp);
   const int blocks = w.tiles_m * w.tiles_n;
-  // ~1024 GEMM workgroups in flight, but at least 16 pixel tiles (512 pixels) per split
-  int splits = std::max(1, std::min(cdiv(w.nkt, 16), cdiv(1024, blocks)));
+  // ~1024 GEMM workgroups in flight, but at least 512 pixels per split
+  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(1024, blocks)));
   w.kt_per_split = cdiv(w.nkt, splits);
   w.splits = cdiv(w.nkt, w.kt_per_split);
   return w;
 }
 
+template <typename T, int KS, int KP, int NW, int OCC>
+static void launch_wgrad_v(const TTParams& p, int bm, int bn, dim3 grid, hipStream_t st) {
+  // 64-row tiles keep 4 waves (2 x 2 of 32 x 32 wave tiles)
+  if (bm == 64 && bn == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 64, KP, 4, OCC>), grid, dim3(256), 0, st, p);
+  else if (bm == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 128, KP, 4, OCC>), grid, dim3(256), 0, st, p);
+  else if (bn == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 64, KP, NW, OCC>), grid, dim3(NW * 64), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 128, KP, NW, OCC>), grid, dim3(NW * 64), 0, st, p);
+}
+
 template <typename T, int KS>
-static void launch_wgrad(const TTParams& p, int bm, int bn, dim3 grid, hipStream_t st) {
-  if (bm == 64 && bn == 64) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 64>), grid, dim3(256), 0, st, p);
-  else if (bm == 64) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 128>), grid, dim3(256), 0, st, p);
-  else if (bn == 64) hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 64>), grid, dim3(256), 0, st, p);
-  else hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 128>), grid, dim3(256), 0, st, p);
+static void launch_wgrad(const TTParams& p, int var, int bm, int bn, dim3 grid, hipStream_t st) {
+  if constexpr (sizeof(T) == 4) {
+    (void)var;
+    launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
+  } else {
+    if (var == 1) launch_wgrad_v<T, KS, 64, 4, 2>(p, bm, bn, grid, st);
+    else if (var == 2) launch_wgrad_v<T, KS, 64, 8, 1>(p, bm, bn, grid, st);
+    else if (var == 3) launch_wgrad_v<T, KS, 32, 8, 2>(p, bm, bn, grid, st);
+    else launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
+  }
 }
 
 }  // namespace yms
@@ -1553,14 +1602,21 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
   p.slab_rows = w.slab_rows; p.slab_ld = w.slab_ld;
   p.div_ow = make_fastdiv(s->wo);
   p.div_ohw = make_fastdiv(s->ho * s->wo);
+  {
+    const long es = elem_size(s->dtype);
+    const long dzb = (long)p.M * dz_ld * es, xb = (long)s->n * s->h * s->w * x_ld * es;
+    if (dzb >= (1l << 31) - (1l << 20) || xb >= (1l << 31) - (1l << 20)) return YMS_ERR_UNSUPPORTED;
+    p.dz_bytes = (uint32_t)dzb;
+    p.x_bytes = (uint32_t)xb;
+  }
   hipStream_t st = (hipStream_t)stream;
   dim3 grid((unsigned)(w.tiles_m * w.tiles_n), (unsigned)w.splits);
   if (s->dtype == YMS_BF16) {
-    if (s->k == 1) launch_wgrad<bf16, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<bf16, 3>(p, w.bm, w.bn, grid, st);
+    if (s->k == 1) launch_wgrad<bf16, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<bf16, 3>(p, w.var, w.bm, w.bn, grid, st);
   } else if (s->dtype == YMS_F16) {
-    if (s->k == 1) launch_wgrad<f16, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<f16, 3>(p, w.bm, w.bn, grid, st);
+    if (s->k == 1) launch_wgrad<f16, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<f16, 3>(p, w.var, w.bm, w.bn, grid, st);
   } else {
-    if (s->k == 1) launch_wgrad<float, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<float, 3>(p, w.bm, w.bn, grid, st);
+    if (s->k == 1) launch_wgrad<float, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<float, 3>(p, w.var, w.bm, w.bn, grid, st);
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
