@@ -129,3 +129,46 @@ def test_invalid_arguments_rejected():
     st = L.lib().yms_conv_fwd(ctypes.pointer(sh), 1, 12, 0, 1, 1, 8, 0, None, None, 0, None, 0, 0, None,
                               L.stream_ptr())
     assert st == 1   # ld not a multiple of 8
+
+
+# full-size tiles: 256-row tiles with BN statistics per 128 rows (M not a multiple of 256),
+# multi-split wgrad
+BIG = [(3, 32, 40, 40, 32, 3, 1), (2, 64, 40, 40, 64, 3, 1), (2, 128, 20, 30, 128, 1, 1),
+       (2, 64, 40, 40, 128, 3, 2)]
+
+
+@pytest.mark.parametrize("shp", BIG)
+def test_conv_bf16_large_tiles(shp):
+    n, cin, h, w, cout, k, s = shp
+    dtype = torch.bfloat16
+    g = torch.Generator().manual_seed(5)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    y, st = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, stats=True)
+    z = ref_conv(x, wt, s, dtype)
+    _close(nchw(y, cout).cpu(), z, TOL["bf16"])
+    _close(st[:, 0, :cout].double().sum(0).cpu().float(), z.sum((0, 2, 3)), 1e-3)
+    _close(st[:, 1, :cout].double().sum(0).cpu().float(), (z * z).sum((0, 2, 3)), 1e-3)
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh_ = torch.randn(cout, generator=g) * 0.1
+    ya, _ = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, sc.cuda(), sh_.cuda(), L.ACT_SILU)
+    _close(nchw(ya, cout).cpu(), F.silu(z * sc.view(1, -1, 1, 1) + sh_.view(1, -1, 1, 1)), TOL["bf16"])
+    dz = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+    xr = x.to(dtype).float().requires_grad_(True)
+    wr = wt.to(dtype).float().requires_grad_(True)
+    F.conv2d(xr, wr, None, s, k // 2).backward(dz.to(dtype).float())
+    sp = ctypes.pointer(shp_)
+    dx = nhwc(torch.zeros(n, cin, h, w), dtype)
+    wpt = pack(wt, shp_, dtype, 1)
+    dzb = nhwc(dz, dtype)
+    L.call("yms_conv_dgrad", sp, dzb.data_ptr(), dzb.shape[-1], 0, wpt.data_ptr(), dx.data_ptr(), dx.shape[-1], 0,
+           0, L.stream_ptr())
+    _close(nchw(dx, cin).cpu(), xr.grad, TOL["bf16"] * 2)
+    xb = nhwc(x, dtype)
+    wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
+    ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device="cuda")
+    dw = torch.zeros(cout, cin, k, k, device="cuda")
+    L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0, ws.data_ptr(),
+           wsb, dw.data_ptr(), 0, L.stream_ptr())
+    _close(dw.cpu(), wr.grad, 2e-3)

@@ -501,7 +501,13 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
   constexpr int RED = (EPI == EPI_STATS) ? WGM * 2 * BN * 4 : 0;
   constexpr int PRM = (EPI == EPI_AFFINE) ? 2 * NTP_MAX_AFFINE_COLS * 4 : 0;
   static_assert((B_PART || BN % RPP == 0) && BM % RPP == 0 && BN <= NTHR, "tile");
-  static_assert(BM * BN * (int)sizeof(T) <= STAGE, "staging must fit one ring stage");
+  // the output tile is staged through the ring stage just consumed, in NH passes of HR rows
+  constexpr int NH = (BM * BN * (int)sizeof(T) > STAGE) ? 2 : 1;
+  constexpr int HR = BM / NH;
+  static_assert(HR * BN * (int)sizeof(T) <= STAGE && HR % (BM / WGM) == 0, "staging must fit one ring stage");
+  // BN statistics: one [2][ld] row per 128 output rows (yms_conv_stats_rows), whatever BM is
+  constexpr int SROWS = BM / 128 > 0 ? BM / 128 : 1;
+  static_assert(BM % 128 == 0 && WGM % SROWS == 0, "statistics rows");
   __shared__ __attribute__((aligned(16))) char smem[ST * STAGE + RED + PRM + 16];
   float* red = reinterpret_cast<float*>(smem + ST * STAGE);
   float* prm = reinterpret_cast<float*>(smem + ST * STAGE + RED);   // [scale | shift] per column
@@ -738,63 +744,75 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
           }
       }
     }
-    lds_barrier();      // every wave has finished reading `stage` as MFMA operands
-#pragma unroll
-    for (int a = 0; a < TM; ++a)
-#pragma unroll
-      for (int b = 0; b < TN; ++b)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          const int rl = wm * WTM + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
-          stg[rl * BN + wn * WTN + b * 32 + lr] = (T)acc[a][b][i];
-          acc[a][b][i] = 0.0f;
-        }
-    lds_barrier();
-    if constexpr (EPI == EPI_STATS) {
-      if (tid < BN) {
-        float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-        for (int w = 0; w < WGM; ++w) {
-          t1 += red[(w * 2 + 0) * BN + tid];
-          t2 += red[(w * 2 + 1) * BN + tid];
-        }
-        float* so = p.stats + (long)tile_m * 2 * p.stats_ld;
-        so[n0 + tid] = t1;
-        so[p.stats_ld + n0 + tid] = t2;
-      }
-    }
     constexpr int CH = BN / 8;      // 16-B chunks per staged row
     constexpr int RS = NTHR / CH;   // rows per pass
     const int ch = tid % CH, rr = tid / CH;
     const int col0 = n0 + ch * 8;
     const int nv = p.Ncols - col0;
 #pragma unroll
-    for (int j = 0; j < BM / RS; ++j) {
-      const int rl = rr + RS * j;
-      int row = m0 + rl;
-      if (row >= M || nv <= 0) continue;
-      float v[8];
-      unpack8(*reinterpret_cast<const Raw8<T>*>(stg + rl * BN + ch * 8), v);
-      if (MODE == MODE_DGRAD2) {
-        const uint32_t n = fdiv((uint32_t)row, dv_hw);
-        const uint32_t rem = (uint32_t)row - n * dv_hw.d;
-        const uint32_t ya = fdiv(rem, dv_w);
-        const uint32_t xb = rem - ya * dv_w.d;
-        row = ((int)n * p.OH + 2 * (int)ya + (cls >> 1)) * p.OWx + 2 * (int)xb + (cls & 1);
-      }
-      T* dst = reinterpret_cast<T*>(p.dst) + (long)row * p.dst_ld + p.dst_off + col0;
-      if (EPI == EPI_AFFINE && p.res) {
-        float r[8];
-        load8(reinterpret_cast<const T*>(p.res) + (long)row * p.res_ld + p.res_off + col0, nv, r);
+    for (int h = 0; h < NH; ++h) {
+      // h = 0: every wave has finished reading `stage` as MFMA operands; h > 0: every thread
+      // has finished reading the previous pass out of the staging rows
+      lds_barrier();
+      if (NH == 1 || (wm * WTM) / HR == h) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += r[i];
-      } else if (EPI == EPI_ACCUM) {
-        float r[8];
-        load8(dst, nv, r);
+        for (int a = 0; a < TM; ++a)
 #pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] += r[i];
+          for (int b = 0; b < TN; ++b)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+              const int rl = wm * WTM - h * HR + a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh;
+              stg[rl * BN + wn * WTN + b * 32 + lr] = (T)acc[a][b][i];
+              acc[a][b][i] = 0.0f;
+            }
       }
-      store8(dst, nv, v);
+      lds_barrier();
+      if constexpr (EPI == EPI_STATS) {
+        if (h == 0 && tid < BN * SROWS) {
+          const int sr = tid / BN, c = tid - sr * BN;
+          constexpr int WPR = WGM / SROWS;    // wave rows per statistics row
+          float t1 = 0.f, t2 = 0.f;
+#pragma unroll
+          for (int w = 0; w < WPR; ++w) {
+            t1 += red[((sr * WPR + w) * 2 + 0) * BN + c];
+            t2 += red[((sr * WPR + w) * 2 + 1) * BN + c];
+          }
+          const int srow = tile_m * SROWS + sr;
+          if (srow * 128 < M) {
+            float* so = p.stats + (long)srow * 2 * p.stats_ld;
+            so[n0 + c] = t1;
+            so[p.stats_ld + n0 + c] = t2;
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < HR / RS; ++j) {
+        const int rl = rr + RS * j;
+        int row = m0 + h * HR + rl;
+        if (row >= M || nv <= 0) continue;
+        float v[8];
+        unpack8(*reinterpret_cast<const Raw8<T>*>(stg + rl * BN + ch * 8), v);
+        if (MODE == MODE_DGRAD2) {
+          const uint32_t n = fdiv((uint32_t)row, dv_hw);
+          const uint32_t rem = (uint32_t)row - n * dv_hw.d;
+          const uint32_t ya = fdiv(rem, dv_w);
+          const uint32_t xb = rem - ya * dv_w.d;
+          row = ((int)n * p.OH + 2 * (int)ya + (cls >> 1)) * p.OWx + 2 * (int)xb + (cls & 1);
+        }
+        T* dst = reinterpret_cast<T*>(p.dst) + (long)row * p.dst_ld + p.dst_off + col0;
+        if (EPI == EPI_AFFINE && p.res) {
+          float r[8];
+          load8(reinterpret_cast<const T*>(p.res) + (long)row * p.res_ld + p.res_off + col0, nv, r);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] += r[i];
+        } else if (EPI == EPI_ACCUM) {
+          float r[8];
+          load8(dst, nv, r);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) v[i] += r[i];
+        }
+        store8(dst, nv, v);
+      }
     }
   };
 
@@ -1271,23 +1289,24 @@ template <typename T, int KS, int MODE, int EPI, bool UNI>
 static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st) {
   NTParams p = p0;
   static const int variant = getenv("YMS_NT_VARIANT") ? atoi(getenv("YMS_NT_VARIANT")) : 0;
-  // 8-wave blocks at 2-3 blocks per CU: 4-6 waves per SIMD hide the ds_read -> MFMA and barrier
-  // latencies that a 4-wave block at 2/CU exposes (1.6-2x measured on the 3x3 layers).
+  // 8-wave blocks at 2-3 per CU (4-6 waves per SIMD) hide the ds_read -> MFMA and barrier
+  // latencies that 4-wave blocks expose; variant 6 (dev A/B): 256-row tiles of 16 waves at
+  // 1 block per CU (25% fewer LDS-fill bytes per FLOP, 2 k-tiles in flight).
   if (cfg == 0) {
     p.tiles_n = cdiv(p.Ncols, 128);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, 2, 512);
+    if (variant == 6)
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1>, p, 256, gy, st, 1, 1024);
+    else
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, 2, 512);
   } else if (cfg == 1) {
     p.tiles_n = cdiv(p.Ncols, 64);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, 3, 512);
-  } else if (MODE == MODE_FWD && variant == 4) {
-    p.tiles_n = cdiv(p.Ncols, 32);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, 2, 512);
-  } else if (MODE == MODE_FWD && variant == 5) {
-    p.tiles_n = cdiv(p.Ncols, 32);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 3, UNI, 2>, p, 256, gy, st, 2, 512);
+    if (variant == 6)
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 64, 8, 2, 3, UNI, 1>, p, 256, gy, st, 1, 1024);
+    else
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, 3, 512);
   } else {
     p.tiles_n = cdiv(p.Ncols, 32);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3, UNI>, p, 128, gy, st, 2, 256);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, 2, 512);
   }
 }
 
