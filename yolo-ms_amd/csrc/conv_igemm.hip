@@ -861,6 +861,7 @@ struct TTParams {
   uint32_t dz_bytes, x_bytes;   // raw-buffer extents of dz and x (< 2^31)
   int kt_per_split;
   int tiles_n;   // kf tiles
+  int tiles_m_n; // row tiles x kf tiles
   int slab_rows, slab_ld;
   FastDiv div_ow, div_ohw;
 };
@@ -897,9 +898,14 @@ __global__ __launch_bounds__(NW * 64, OCC) void conv_wgrad_kernel(TTParams p) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
-  const int wg = xcd_remap(blockIdx.x, gridDim.x);
+  // 1-D grid, split-major logical order: the tiles sharing a pixel split (its dz rows and x
+  // im2col columns) are consecutive logical ids, which xcd_remap keeps on one XCD's L2
+  const int tmn = p.tiles_m_n;
+  // (measured: grouping pays from 4 tiles per split up; below that plain dispatch order is faster)
+  const int lid = tmn >= 4 ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int wg = lid % tmn;
   const int tile_n = wg % p.tiles_n, tile_m = wg / p.tiles_n;
-  const int split = blockIdx.y;
+  const int split = lid / tmn;
   const int m0 = tile_m * BM, n0 = tile_n * BN;
   const int kt0 = split * p.kt_per_split;
   const int kt1 = min(p.nkt, kt0 + p.kt_per_split);
@@ -1392,8 +1398,9 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   const long M = (long)s->n * s->ho * s->wo;
   w.nkt = cdiv(M, w.kp);
   const int blocks = w.tiles_m * w.tiles_n;
-  // ~1024 GEMM workgroups in flight, but at least 512 pixels per split
-  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(1024, blocks)));
+  // about 4 workgroups per CU (2-4 resident by LDS), at least 512
+  // pixels per split
+  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(4 * cu_count(), blocks)));
   w.kt_per_split = cdiv(w.nkt, splits);
   w.splits = cdiv(w.nkt, w.kt_per_split);
   return w;
@@ -1629,7 +1636,8 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
     p.x_bytes = (uint32_t)xb;
   }
   hipStream_t st = (hipStream_t)stream;
-  dim3 grid((unsigned)(w.tiles_m * w.tiles_n), (unsigned)w.splits);
+  p.tiles_m_n = w.tiles_m * w.tiles_n;
+  dim3 grid((unsigned)(w.tiles_m * w.tiles_n * w.splits));
   if (s->dtype == YMS_BF16) {
     if (s->k == 1) launch_wgrad<bf16, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<bf16, 3>(p, w.var, w.bm, w.bn, grid, st);
   } else if (s->dtype == YMS_F16) {
