@@ -1,7 +1,7 @@
 #!/bin/bash
 # Profile the bench command on a GPU box (run through gpurun from the repo root):
 #   tools/profile_round.sh r01
-# 1) rocprofv3 --kernel-trace --stats of the default bench (train + infer) -> per-kernel times
+# 1) rocprofv3 --kernel-trace --stats of bench.py --mode train and --mode infer -> per-kernel times
 # 2-4) separate PMC passes (FETCH_SIZE | WRITE_SIZE | MFMA busy) of a short bench run
 # Outputs under gpurun_out/<tag>/; copy the summaries into profiles/ afterwards.
 set -e
@@ -10,8 +10,10 @@ ROOT=${GRAFT_REPO_ROOT:-$(pwd)}
 OUT=$ROOT/gpurun_out/$TAG
 mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats" -o run -- \
-  python3 "$ROOT/bench.py" --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench.json" 2> "$OUT/bench.err"
+for mode in train infer; do
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$mode" -o run -- \
+    python3 "$ROOT/bench.py" --mode $mode --steps 10 --warmup 3 --no-cpu-baseline > "$OUT/bench_$mode.json" 2> "$OUT/bench_$mode.err"
+done
 echo "stats done"
 # PMC passes per mode (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950)
 for mode in train infer; do
@@ -29,7 +31,9 @@ cd "$ROOT"
 for e in "$OUT"/*.err; do echo "== $e"; grep -v "^[EWI]2026\|^[EWI][0-9]\{8\}" "$e" | tail -5; done
 ls -la "$OUT"/*/ | head -40
 du -sh "$OUT"/* > "$OUT/sizes.txt" || true
-python3 tools/rocprof_summary.py stats "$OUT/stats/run_kernel_stats.csv" > "$OUT/stats_summary.txt"
+for mode in train infer; do
+  python3 tools/rocprof_summary.py stats "$OUT/stats_$mode/run_kernel_stats.csv" > "$OUT/stats_${mode}_summary.txt"
+done
 python3 tools/rocprof_summary.py traffic "$OUT" > "$OUT/pmc_traffic.json"
 find "$OUT" -name "*.db" -delete
 for f in $(find "$OUT" -name "*.csv" -size +4M); do head -c 200000 "$f" > "$f.head"; rm -f "$f"; done

@@ -32,9 +32,9 @@ def family(name):
     if m:
         return "conv_fwd" if int(m.group(4)) <= 1 else "conv_dgrad"
     m = re.search(r"conv_ntp?_kernel<(.*)>", name)
-    if m:   # demangled (rocprof mangles T/KS oddly): count from the end; ntp has a trailing ST
-        args = m.group(1).split(",")
-        epi = int(args[-6 if "conv_ntp" in name else -5])
+    if m:   # demangled (rocprof garbles T/KS): MODE and EPI are the first two numeric arguments
+        nums = [a.strip() for a in m.group(1).split(",") if a.strip().isdigit()]
+        epi = int(nums[1])
         return "conv_fwd" if epi <= 1 else "conv_dgrad"
     if "conv_wgrad_kernel" in name or "wgrad_reduce_kernel" in name:
         return "conv_wgrad"
