@@ -315,8 +315,93 @@ __device__ __forceinline__ bool iou_gt_f(const float4& i, const float4& j, float
   const float w = fmaxf(0.0f, xx2 - xx1);
   const float h = fmaxf(0.0f, yy2 - yy1);
   const float inter = w * h;
-  const float ovr = inter / (iarea + jarea - inter);
+  const float u = iarea + jarea - inter;
+  // Decide by one multiply when the ratio is clearly away from the threshold: the margins
+  // (1e-6 relative) dwarf the 2^-24 roundings of thr_f * u and of the reference's quotient, so
+  // the outcome equals fl(inter / u) > thr_f; only near-ties pay the IEEE division.
+  if (u > 0.0f) {
+    const float t = thr_f * u;
+    if (inter > t * 1.000001f) return true;
+    if (inter < t * 0.999999f) return false;
+  }
+  const float ovr = inter / u;
   return ovr > thr_f;
+}
+
+// Ascending bitonic sort of keys[0, n), n <= 8192, by one 1024-thread block.  Thread t keeps
+// keys [8t, 8t + 8) in registers: exchange distances below 8 are in-thread, below 512 lane
+// shuffles, only the rest (10 of the 91 passes at 8192 keys) go through LDS.  Padding = ~0.
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
+  const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
+  return ((uint64_t)hi << 32) | lo;
+}
+template <int M> __device__ __forceinline__ void cas_in_thread(uint64_t (&r)[8]) {
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int q = i ^ M;
+    if (q > i) {
+      const uint64_t a = r[i], b = r[q];
+      r[i] = a < b ? a : b;
+      r[q] = a < b ? b : a;
+    }
+  }
+}
+__device__ void sort8192(uint64_t* keys, int n) {
+  const int tid = threadIdx.x, lane = tid & 63;
+  uint64_t r[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = 8 * tid + i;
+    r[i] = e < n ? keys[e] : ~0ull;
+  }
+  int N2 = 8;
+  while (N2 < n) N2 <<= 1;
+  for (int k = 2; k <= N2; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int m = (j == (k >> 1)) ? (k - 1) : j;   // partner index = e ^ m
+      if (m >= 512) {
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) keys[8 * tid + i] = r[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+          const int e = 8 * tid + i, pe = e ^ m;
+          const uint64_t o = keys[pe];
+          r[i] = (e < pe) == (o < r[i]) ? o : r[i];
+        }
+      } else if (m >= 8) {
+        const int lm = m >> 3;
+        const bool lower = !((lane >> (31 - __clz(lm))) & 1);
+        uint64_t o[8];
+        if (m & 7) {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = shfl_xor64(r[i ^ 7], lm);
+        } else {
+#pragma unroll
+          for (int i = 0; i < 8; ++i) o[i] = shfl_xor64(r[i], lm);
+        }
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] = lower == (o[i] < r[i]) ? o[i] : r[i];
+      } else {
+        switch (m) {
+          case 1: cas_in_thread<1>(r); break;
+          case 2: cas_in_thread<2>(r); break;
+          case 3: cas_in_thread<3>(r); break;
+          case 4: cas_in_thread<4>(r); break;
+          default: cas_in_thread<7>(r); break;
+        }
+      }
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int e = 8 * tid + i;
+    if (e < n) keys[e] = r[i];
+  }
+  __syncthreads();
 }
 
 __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const float* bxy, NmsWs ws) {
@@ -330,6 +415,11 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
     uint64_t* gk = ws.gkeys + (long)b * A + off;
     const bool inlds = n <= NMS_BIG_LDS_KEYS;
     uint64_t* keys = inlds ? s_big : gk;
+    if (n <= 8192) {
+      for (int i = tid; i < n; i += 1024) s_big[i] = gk[i];
+      __syncthreads();
+      sort8192(s_big, n);
+    } else {
     if (inlds)
       for (int i = tid; i < n; i += 1024) s_big[i] = gk[i];
     __syncthreads();
@@ -346,6 +436,7 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
         }
         __syncthreads();
       }
+    }
     }
     float4* boxes = ws.gboxes + (long)b * A + off;
     const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
