@@ -472,11 +472,19 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
     int* idx = ws.scratch + (long)b * A + off;
     if (tid == 0) s_nk = 0;
     __syncthreads();
+    // the next block's candidates are fetched one iteration ahead (their load latency overlaps
+    // this block's tests); compaction only writes slots < blk + 64, so the prefetch is safe
+    float4 cb_nx = lane < n ? boxes[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
+    int cid_nx = lane < n ? idx[lane] : 0;
     for (int blk = 0; blk < n; blk += 64) {
       const int m = min(64, n - blk);
       const bool has = lane < m;
-      const float4 cb = has ? boxes[blk + lane] : make_float4(0.f, 0.f, 0.f, 0.f);
-      const int cid = has ? idx[blk + lane] : 0;
+      const float4 cb = cb_nx;
+      const int cid = cid_nx;
+      if (blk + 64 + lane < n) {
+        cb_nx = boxes[blk + 64 + lane];
+        cid_nx = idx[blk + 64 + lane];
+      }
       const int nk = s_nk;
       bool sup = false;
       if (has) {
