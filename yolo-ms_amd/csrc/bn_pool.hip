@@ -659,11 +659,12 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
   return launch_status();
 }
 
-// pixels per block for the channel-stationary kernels: about two U-pixel iterations per
-// thread, at most 8192 blocks
+// pixels per block for the channel-stationary kernels: about four U-pixel iterations per
+// thread (amortises the per-channel parameter loads; measured best of 1/2/4/8), at most 8192
+// blocks
 static long elem_ppb(long npix, int c) {
   const long py = 256 / ((c + 7) / 8);
-  const long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * 2), 1), 8192);
+  const long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * 4), 1), 8192);
   return (npix + blocks - 1) / blocks;
 }
 
