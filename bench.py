@@ -195,7 +195,9 @@ def main():
         def train_step():
             opt.zero_grad(set_to_none=True)
             outs = net(x)
-            loss = sum((o.float() ** 2).mean() for o in outs)   # surrogate
+            # surrogate sum_i mean(o_i^2), as one fp32-accumulating reduction per
+            # head map instead of materialising an fp32 copy and its square
+            loss = sum(torch.linalg.vector_norm(o, dtype=torch.float32).square() / o.numel() for o in outs)
             loss.backward()
             opt.step()
 
