@@ -91,6 +91,22 @@ def conv_roofline(prof, label):
             "algorithmic_gflop_per_launch": round(fl / max(calls, 1) / 1e9, 3)}
 
 
+class MeanSquare(torch.autograd.Function):
+    """mean(o^2) of a head map: forward is one fp32-accumulating norm reduction (no fp32 copy of
+    o), backward writes d/do = 2*o/numel in one elementwise pass (autograd's vector_norm backward
+    takes three: a divide by the norm, a masked fill for norm == 0 and a multiply)."""
+
+    @staticmethod
+    def forward(ctx, o):
+        ctx.save_for_backward(o)
+        return torch.linalg.vector_norm(o, dtype=torch.float32).square() / o.numel()
+
+    @staticmethod
+    def backward(ctx, g):
+        (o,) = ctx.saved_tensors
+        return o * (g * (2.0 / o.numel())).to(o.dtype)
+
+
 def pmc_traffic(mode, workload):
     """HBM bytes per conv call from the newest committed PMC profile of the same workload
     (profiles/*_pmc_traffic.json, written by tools/profile_round.sh + tools/rocprof_summary.py
@@ -195,9 +211,8 @@ def main():
         def train_step():
             opt.zero_grad(set_to_none=True)
             outs = net(x)
-            # surrogate sum_i mean(o_i^2), as one fp32-accumulating reduction per
-            # head map instead of materialising an fp32 copy and its square
-            loss = sum(torch.linalg.vector_norm(o, dtype=torch.float32).square() / o.numel() for o in outs)
+            # surrogate sum_i mean(o_i^2)
+            loss = sum(MeanSquare.apply(o) for o in outs)
             loss.backward()
             opt.step()
 

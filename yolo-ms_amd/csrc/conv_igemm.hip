@@ -883,7 +883,8 @@ __device__ __forceinline__ u32x4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t voff) 
 template <typename T, int KS, int BM, int BN, int KP, int NW, int OCC>
 __global__ __launch_bounds__(NW * 64, OCC) void conv_wgrad_kernel(TTParams p) {
   constexpr int NTHR = NW * 64;
-  constexpr int WGN = (NW == 8 && BN >= 128) ? 4 : 2, WGM = NW / WGN;
+  // 32-row tiles (cout <= 32) lay all waves along the kf columns
+  constexpr int WGN = BM == 32 ? NW : (NW == 8 && BN >= 128) ? 4 : 2, WGM = NW / WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0 && KP % 16 == 0, "wgrad tile");
@@ -1387,7 +1388,7 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   w.cpt = w.cin8 * es / 16;
   w.kc = s->k * s->k * w.cpt;
   const int kf = s->k * s->k * w.cin8;
-  w.bm = s->cout <= 64 ? 64 : 128;
+  w.bm = s->cout <= 32 ? 32 : s->cout <= 64 ? 64 : 128;
   w.bn = kf <= 64 ? 64 : 128;
   w.tiles_m = cdiv(s->cout, w.bm);
   w.tiles_n = cdiv(kf, w.bn);
@@ -1408,8 +1409,12 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
 
 template <typename T, int KS, int KP, int NW, int OCC>
 static void launch_wgrad_v(const TTParams& p, int bm, int bn, dim3 grid, hipStream_t st) {
-  // 64-row tiles keep 4 waves (2 x 2 of 32 x 32 wave tiles)
-  if (bm == 64 && bn == 64)
+  // 32-row tiles: 2 / 4 waves of 32 x 32 along kf; 64-row tiles keep 4 waves (2 x 2)
+  if (bm == 32 && bn == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 32, 64, KP, 2, OCC>), grid, dim3(128), 0, st, p);
+  else if (bm == 32)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 32, 128, KP, 4, OCC>), grid, dim3(256), 0, st, p);
+  else if (bm == 64 && bn == 64)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 64, KP, 4, OCC>), grid, dim3(256), 0, st, p);
   else if (bm == 64)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 128, KP, 4, OCC>), grid, dim3(256), 0, st, p);
