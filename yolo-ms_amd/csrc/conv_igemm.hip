@@ -883,15 +883,17 @@ __device__ __forceinline__ u32x4 bld16(__amdgpu_buffer_rsrc_t r, uint32_t voff) 
 template <typename T, int KS, int BM, int BN, int KP, int NW, int OCC>
 __global__ __launch_bounds__(NW * 64, OCC) void conv_wgrad_kernel(TTParams p) {
   constexpr int NTHR = NW * 64;
-  // 32-row tiles (cout <= 32) lay all waves along the kf columns
-  constexpr int WGN = BM == 32 ? NW : (NW == 8 && BN >= 128) ? 4 : 2, WGM = NW / WGN;
+  // 32- and 96-row tiles (cout <= 32, <= 96) lay all waves along the kf columns
+  constexpr int WGN = (BM == 32 || BM == 96) ? NW : (NW == 8 && BN >= 128) ? 4 : 2, WGM = NW / WGN;
   constexpr int WTM = BM / WGM, WTN = BN / WGN;
   constexpr int TM = WTM / 32, TN = WTN / 32;
   static_assert(TM >= 1 && TN >= 1 && WTM % 32 == 0 && WTN % 32 == 0 && KP % 16 == 0, "wgrad tile");
   constexpr int SZ = sizeof(T);
   constexpr bool F32 = SZ == 4;
   constexpr int EPC = 16 / SZ;                 // elements per chunk
-  constexpr int PA = BM * SZ + 64, PB = BN * SZ + 64;   // LDS pitches (conflict-free tr reads)
+  // LDS pitches (conflict-free tr reads: a pitch that is a multiple of the 256-B bank span
+  // would put the 4 rows one tr-read group touches on the same banks)
+  constexpr int PA = BM * SZ + ((BM * SZ + 64) % 256 == 0 ? 128 : 64), PB = BN * SZ + 64;
   constexpr int CA = BM / EPC, CB = BN / EPC;  // chunks per LDS row
   constexpr int A_SLOTS = (KP * CA + NTHR - 1) / NTHR, B_SLOTS = (KP * CB + NTHR - 1) / NTHR;
   constexpr int TILE = KP * (PA + PB);
@@ -1388,20 +1390,21 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   w.cpt = w.cin8 * es / 16;
   w.kc = s->k * s->k * w.cpt;
   const int kf = s->k * s->k * w.cin8;
-  w.bm = s->cout <= 32 ? 32 : s->cout <= 64 ? 64 : 128;
+  w.bm = s->cout <= 32 ? 32 : s->cout <= 64 ? 64 : s->cout <= 96 ? 96 : 128;
   w.bn = kf <= 64 ? 64 : 128;
   w.tiles_m = cdiv(s->cout, w.bm);
   w.tiles_n = cdiv(kf, w.bn);
   w.slab_rows = w.tiles_m * w.bm;
   w.slab_ld = w.tiles_n * w.bn;
   w.var = wgrad_variant(s->dtype);
-  w.kp = (w.var == 1 || w.var == 2) ? 64 : 32;
+  w.kp = 32;
   const long M = (long)s->n * s->ho * s->wo;
   w.nkt = cdiv(M, w.kp);
   const int blocks = w.tiles_m * w.tiles_n;
   // about 4 workgroups per CU (2-4 resident by LDS), at least 512
   // pixels per split
-  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(4 * cu_count(), blocks)));
+  static const int wpc = getenv("YMS_WG_WPC") ? std::max(1, atoi(getenv("YMS_WG_WPC"))) : 4;
+  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(wpc * cu_count(), blocks)));
   w.kt_per_split = cdiv(w.nkt, splits);
   w.splits = cdiv(w.nkt, w.kt_per_split);
   return w;
@@ -1414,6 +1417,10 @@ static void launch_wgrad_v(const TTParams& p, int bm, int bn, dim3 grid, hipStre
     hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 32, 64, KP, 2, OCC>), grid, dim3(128), 0, st, p);
   else if (bm == 32)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 32, 128, KP, 4, OCC>), grid, dim3(256), 0, st, p);
+  else if (bm == 96 && bn == 64)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 96, 64, KP, 2, OCC>), grid, dim3(128), 0, st, p);
+  else if (bm == 96)
+    hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 96, 128, KP, 4, OCC>), grid, dim3(256), 0, st, p);
   else if (bm == 64 && bn == 64)
     hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 64, 64, KP, 4, OCC>), grid, dim3(256), 0, st, p);
   else if (bm == 64)
@@ -1430,8 +1437,8 @@ static void launch_wgrad(const TTParams& p, int var, int bm, int bn, dim3 grid, 
     (void)var;
     launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
   } else {
-    if (var == 1) launch_wgrad_v<T, KS, 64, 4, 2>(p, bm, bn, grid, st);
-    else if (var == 2) launch_wgrad_v<T, KS, 64, 8, 1>(p, bm, bn, grid, st);
+    if (var == 1) launch_wgrad_v<T, KS, 32, 4, 4>(p, bm, bn, grid, st);
+    else if (var == 2) launch_wgrad_v<T, KS, 32, 4, 3>(p, bm, bn, grid, st);
     else if (var == 3) launch_wgrad_v<T, KS, 32, 8, 2>(p, bm, bn, grid, st);
     else launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
   }
