@@ -63,7 +63,10 @@ def _worker(rank, world, port, q):
             bk.begin(plan, pg, None, views)
             for op in reversed(plan.ops):
                 # a bucket must only be launched once all its params are written
+                before = bk.launched_buckets
+                will = bk.pending(op)
                 bk.op_done(op)
+                assert will == (bk.launched_buckets > before)
             launched.append(bk.launched_buckets)
             bk.finish()
         exp = []

@@ -1,5 +1,6 @@
 """Per-layer conv timing vs roofline for one forward (and optionally train step) (dev tool)."""
 import os, sys, ctypes
+os.environ.setdefault("YMS_WGRAD_STREAM", "0")   # events below are recorded on the current stream
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "yolo-ms_amd")]
 import torch

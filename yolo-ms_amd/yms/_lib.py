@@ -124,9 +124,12 @@ def call(name, *args):
         return
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
-    s.record()
+    # conv entry points take their hipStream_t last: time them on the stream they run on
+    # (wgrad runs on the backward's side stream)
+    st = torch.cuda.ExternalStream(args[-1]) if name in _CONV and args[-1] else None
+    s.record(st)
     check(getattr(lib(), name)(*args), name)
-    e.record()
+    e.record(st)
     fl = 0
     if name in _CONV:
         sh = args[0].contents
@@ -135,7 +138,8 @@ def call(name, *args):
 
 
 def profile_begin():
-    """Record a HIP event pair around every C-ABI launch on the current stream (diagnostic)."""
+    """Record a HIP event pair around every C-ABI launch (diagnostic): conv launches on the
+    stream they are issued to, everything else on the current stream."""
     global _prof
     _prof = []
 

@@ -79,6 +79,10 @@ class GradBucketer:
             return dist.all_reduce(t, op=dist.ReduceOp.AVG, group=self.group, async_op=True)
         return dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
 
+    def pending(self, op):
+        """True when op_done(op) will launch a bucket all-reduce."""
+        return bool(self.ready.get(self.pos[id(op)]))
+
     def op_done(self, op):
         for bi in self.ready.get(self.pos[id(op)], ()):
             a, b, _ = self.buckets[bi]

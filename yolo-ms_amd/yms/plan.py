@@ -147,12 +147,25 @@ class Rt:
         self.pg_base = None      # flat fp32 param-grad arena pointer
         self.eval_base = None    # eval cache base pointer (packed weights + folded BN)
         self.prepacked = False   # training: all weight packs already issued (Plan.prepack)
+        self.main = None         # backward: torch stream objects (main, weight-gradient side stream)
+        self.side = None
 
     def a(self, v):
         return self.base + v.buf.off
 
     def g(self, v):
         return self.gbase + v.buf.off
+
+    def wst(self):
+        """Stream for a weight-gradient GEMM (+ its split reduce): a side stream ordered after
+        everything enqueued on the main stream so far.  wgrad is off the backward's critical
+        path (only the optimizer consumes dw), so it overlaps the next layers' HBM-bound BN
+        backward kernels and dgrads.  Only wgrads use the side stream, so the shared
+        "wgrad" scratch stays in stream order."""
+        if self.side is None:
+            return self.st
+        self.side.wait_stream(self.main)
+        return self.side.cuda_stream
 
 
 class ConvOp:
@@ -267,7 +280,7 @@ class ConvOp:
         if dw is not None:
             wsz = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
-                   rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.st)
+                   rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
 
     def grad_params(self):
         return [self.pb, self.pg, self.pw]
@@ -336,7 +349,7 @@ class BiasConvOp:
         dw = rt.pgrad(self.pw)
         if dw is not None:
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, gy, gyl, gyo,
-                   rt.gbase + rt.plan.gscratch["wgrad"], L.lib().yms_conv_wgrad_ws_bytes(self.sp), dw, 0, rt.st)
+                   rt.gbase + rt.plan.gscratch["wgrad"], L.lib().yms_conv_wgrad_ws_bytes(self.sp), dw, 0, rt.wst())
 
     def grad_params(self):
         return [self.pbias, self.pw]

@@ -9,6 +9,8 @@ ATen-conv fallback: CPU tensors or a missing libyms.so raise RuntimeError.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -111,6 +113,18 @@ def _seed_grad(plan, rt, v, g, acc):
            v.off, acc, rt.st)
 
 
+# weight-gradient GEMMs on a per-device side stream (YMS_WGRAD_STREAM=0: all on one stream)
+WGRAD_SIDE_STREAM = os.environ.get("YMS_WGRAD_STREAM", "1") != "0"
+_SIDE = {}
+
+
+def _side_stream(dev):
+    s = _SIDE.get(dev)
+    if s is None:
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+    return s
+
+
 L_DTYPES = {L.F32: torch.float32, L.BF16: torch.bfloat16, L.F16: torch.float16}
 
 
@@ -144,6 +158,8 @@ class _PlanFn(torch.autograd.Function):
         plan, rt = state.plan, state.rt
         dev = state.arena.device
         rt.st = L.stream_ptr(dev)
+        rt.main = torch.cuda.current_stream(dev)
+        rt.side = _side_stream(dev) if WGRAD_SIDE_STREAM else None
         garena = torch.empty(max(plan.garena_bytes, 1), dtype=torch.uint8, device=dev)
         rt.gbase = garena.data_ptr()
         for off, nb in plan.gzero_ranges:
@@ -173,7 +189,12 @@ class _PlanFn(torch.autograd.Function):
         for op in reversed(plan.ops):
             op.bwd(rt)
             if hook is not None:
+                if rt.side is not None and hook.pending(op):
+                    rt.main.wait_stream(rt.side)   # the bucket's dw come from side-stream wgrads
                 hook.op_done(op)
+        if rt.side is not None:
+            rt.main.wait_stream(rt.side)
+            rt.side = None
         if hook is not None:
             hook.finish()
         in_grads = []
