@@ -120,3 +120,71 @@ def test_postprocess_dicts():
         assert np.array_equal(r["labels"].cpu().numpy(), kl)
         assert np.array_equal(r["boxes"].cpu().numpy(), bx[ki])
         assert np.array_equal(r["scores"].cpu().numpy(), pred[b, ki, 4:].max(1))
+
+
+# ---- configs[4]: 1280x1280 inputs, A = 33600 anchors ---------------------------------------
+
+def test_1280_single_class_beyond_lds_sort():
+    """nc=1 at A=33600: ~25k candidates in one segment, past the 16384-key LDS sort (global
+    bitonic path) and the kept-list greedy over a long list."""
+    rng = np.random.default_rng(7)
+    A = 33600
+    pred = np.zeros((1, A, 5), np.float32)
+    pred[..., :2] = rng.uniform(0, 1280, (1, A, 2))
+    pred[..., 2:4] = rng.uniform(10, 160, (1, A, 2))
+    pred[..., 4] = rng.uniform(0.0, 1.0, (1, A))
+    pred[0, ::97, 4] = 0.625     # exact score ties across far-apart anchors
+    assert _check(pred, 0.25, 0.5) > 0
+
+
+def test_1280_dense_multiclass():
+    """80 classes, ~all 33600 anchors above conf (~420 per class), two images."""
+    rng = np.random.default_rng(8)
+    A, nc = 33600, 80
+    pred = np.zeros((2, A, 4 + nc), np.float32)
+    pred[..., :2] = rng.uniform(0, 1280, (2, A, 2))
+    pred[..., 2:4] = rng.uniform(10, 240, (2, A, 2))
+    pred[..., 4:] = rng.uniform(0.2, 0.6, (2, A, nc))
+    _check(pred, 0.25, 0.45)
+
+
+def test_s1280_fp16_model_decode_nms_end_to_end():
+    """configs[4] path end to end: random-init YOLO-MS-S, 1280x1280 fp16 forward + decode on the
+    GPU, then class-wise NMS on the GPU vs the C oracle on the same decoded tensor (bit-exact)."""
+    from yolov8.yolov8 import YOLOv8
+    torch.manual_seed(0)
+    m = YOLOv8("s", 80).cuda().eval()
+    m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    x = torch.randn(2, 3, 1280, 1280, generator=torch.Generator().manual_seed(9))
+    with torch.no_grad(), torch.autocast("cuda", dtype=torch.float16):
+        det = m(x.cuda())
+    assert det.shape == (2, 33600, 84) and det.dtype == torch.float32
+    assert _check(np.ascontiguousarray(det.cpu().numpy()), 0.25, 0.45) > 0
+
+
+def test_big_segment_grid_edge_cases():
+    """Big-segment greedy paths: wide boxes (> 64 grid cells, the wide-box list), zero-area and
+    inverted boxes, kept lists beyond the LDS mirror / link pool (fallback to the full kept
+    list), a non-finite coordinate (whole-list path) and a negative threshold."""
+    rng = np.random.default_rng(11)
+    A = 8400
+    def seg(wlo, whi):
+        p = np.zeros((1, A, 5), np.float32)
+        p[..., :2] = rng.uniform(0, 640, (1, A, 2))
+        p[..., 2:4] = rng.uniform(wlo, whi, (1, A, 2))
+        p[..., 4] = rng.uniform(0.3, 1.0, (1, A))
+        return p
+    p = seg(8, 40)
+    p[0, ::50, 2:4] = rng.uniform(300, 900, (len(p[0, ::50]), 2))    # wide boxes
+    p[0, 1::97, 2] = 0.0                                               # zero width
+    p[0, 2::89, 3] = -5.0                                              # inverted (negative h)
+    assert _check(p, 0.25, 0.5) > 0
+    p = seg(0.5, 3.0)                     # tiny, nearly disjoint: ~all kept (> 4096)
+    assert _check(p, 0.25, 0.5) > 4096
+    p = seg(8, 40)
+    p[0, 123, 0] = np.nan
+    _check(p, 0.25, 0.5)
+    p = seg(8, 40)
+    p[0, 77, 1] = np.inf
+    _check(p, 0.25, 0.5)
+    _check(seg(8, 40), 0.25, -0.5)

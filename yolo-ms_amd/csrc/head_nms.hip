@@ -451,17 +451,54 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
 }
 
 // Greedy suppression over a sorted big segment, one 1024-thread block per segment: candidates
-// are taken in 64-blocks; all 16 waves test the block against the boxes kept so far (kept list
-// compacted to the front of the segment's sorted box array, read through L1/L2), then wave 0
-// resolves the block itself in score order, visiting only the still-alive candidates.  Work
-// is O(candidates x kept): a random-init model's near-identical boxes keep a few hundred of
-// 6400 candidates, where an all-pairs bitmask would cost 20M IoUs per segment.
-constexpr int NMS_KEPT_LDS = 6144;   // kept boxes mirrored in LDS (96 KB dynamic); beyond: global
+// are taken in 64-blocks; all 16 waves test the block against the boxes kept so far, then wave 0
+// resolves the block itself in score order, visiting only the still-alive candidates.
+//
+// Kept boxes are bucketed on a per-segment Gx x Gy grid (cell ~ the mean box size): a kept box is
+// linked into every cell its [x1,x2] x [y1,y2] range maps to, and a candidate tests only the
+// lists of the cells its own range maps to (plus a list of boxes spanning > 64 cells).  Exact: a
+// positive intersection has a = max(x1_i, x1_j) inside both x-ranges, and the cell map
+// f(v) = clamp(floor((v - ox) * inv)) is monotone in v, so f(a) lies in both cell ranges (same
+// for y); a is an input coordinate, so no rounding enters the argument.  Zero-area and inverted
+// boxes never take part in a positive intersection (iou_gt_f returns false), so they are not
+// linked and are never tested.  The segment falls back to testing the whole kept list (the
+// pre-grid algorithm) for a negative threshold (`full`), a non-finite coordinate, or once the
+// LDS kept mirror / link pool is full.
+constexpr int NMS_KEPT_LDS = 4096;   // kept boxes mirrored in LDS (64 KB); beyond: global
+constexpr int NMS_LINKS = 10240;     // (kept index, next) link pool (80 KB)
+constexpr int NMS_GMAX = 32;         // grid side cap; head slot NMS_GMAX^2 = the wide-box list
+constexpr size_t NMS_GREEDY_LDS =
+    (size_t)NMS_KEPT_LDS * 16 + (size_t)NMS_LINKS * 8 + (size_t)(NMS_GMAX * NMS_GMAX + 1) * 4;
+
+__device__ __forceinline__ int nms_cell(float v, float o, float inv, int g) {
+  float f = (v - o) * inv;
+  f = fminf(fmaxf(f, 0.0f), (float)(g - 1));
+  return (int)f;
+}
+
+__device__ __forceinline__ float wave_min(float v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v = fminf(v, __shfl_xor(v, m));
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v = fmaxf(v, __shfl_xor(v, m));
+  return v;
+}
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int m = 32; m > 0; m >>= 1) v += __shfl_xor(v, m);
+  return v;
+}
 
 __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
-  extern __shared__ float4 s_kept[];   // [NMS_KEPT_LDS]
+  extern __shared__ float4 s_kept[];                              // [NMS_KEPT_LDS]
+  int2* s_link = reinterpret_cast<int2*>(s_kept + NMS_KEPT_LDS);  // [NMS_LINKS] (kept idx, next)
+  int* s_head = reinterpret_cast<int*>(s_link + NMS_LINKS);       // [NMS_GMAX^2 + 1]
   __shared__ unsigned long long s_sup[16];
-  __shared__ int s_nk;
+  __shared__ float s_red[7][16];
+  __shared__ int s_nk, s_nlink, s_ovf;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbig = ws.big[0];
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
@@ -470,8 +507,57 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
     const int off = ws.cls_off[(long)b * nc + c];
     float4* boxes = ws.gboxes + (long)b * A + off;
     int* idx = ws.scratch + (long)b * A + off;
-    if (tid == 0) s_nk = 0;
+    // ---- segment extent, mean box size and finiteness (over the positive-area boxes) ----
+    {
+      float mnx = INFINITY, mny = INFINITY, mxx = -INFINITY, mxy = -INFINITY, sw = 0.f, sh = 0.f, cnt = 0.f;
+      bool bad = false;
+      for (int i = tid; i < n; i += 1024) {
+        const float4 q = boxes[i];
+        if (!(isfinite(q.x) && isfinite(q.y) && isfinite(q.z) && isfinite(q.w))) {
+          bad = true;
+        } else if (q.z > q.x && q.w > q.y) {
+          mnx = fminf(mnx, q.x); mny = fminf(mny, q.y);
+          mxx = fmaxf(mxx, q.z); mxy = fmaxf(mxy, q.w);
+          sw += q.z - q.x; sh += q.w - q.y; cnt += 1.f;
+        }
+      }
+      mnx = wave_min(mnx); mny = wave_min(mny); mxx = wave_max(mxx); mxy = wave_max(mxy);
+      sw = wave_sum(sw); sh = wave_sum(sh); cnt = wave_sum(cnt);
+      const bool wbad = __ballot(bad) != 0ull;
+      if (lane == 0) {
+        s_red[0][wave] = mnx; s_red[1][wave] = mny; s_red[2][wave] = mxx; s_red[3][wave] = mxy;
+        s_red[4][wave] = sw; s_red[5][wave] = sh; s_red[6][wave] = wbad ? 1.f : cnt;
+        if (wbad) s_red[6][wave] = -1.f;
+      }
+    }
+    for (int i = tid; i <= NMS_GMAX * NMS_GMAX; i += 1024) s_head[i] = -1;
+    if (tid == 0) { s_nk = 0; s_nlink = 0; s_ovf = 0; }
     __syncthreads();
+    float ox = INFINITY, oy = INFINITY, ex = -INFINITY, ey = -INFINITY, sw = 0.f, sh = 0.f, cnt = 0.f;
+    bool bad = false;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      ox = fminf(ox, s_red[0][q]); oy = fminf(oy, s_red[1][q]);
+      ex = fmaxf(ex, s_red[2][q]); ey = fmaxf(ey, s_red[3][q]);
+      sw += s_red[4][q]; sh += s_red[5][q];
+      if (s_red[6][q] < 0.f) bad = true; else cnt += s_red[6][q];
+    }
+    bool grid = !full && !bad;           // block-uniform
+    int gx = 1, gy = 1;
+    float invx = 0.f, invy = 0.f;
+    if (grid && cnt > 0.f) {
+      const float wx = ex - ox, wy = ey - oy, mw = sw / cnt, mh = sh / cnt;
+      // cell ~ half the mean box: a candidate spans ~3x3 cells, spread over 9 waves
+      gx = (int)fminf(fmaxf(2.f * wx / fmaxf(mw, 1e-30f), 1.f), (float)NMS_GMAX);
+      gy = (int)fminf(fmaxf(2.f * wy / fmaxf(mh, 1e-30f), 1.f), (float)NMS_GMAX);
+      invx = (float)gx / wx;
+      invy = (float)gy / wy;
+      if (!(invx < 1e30f)) invx = 0.f;   // inf / NaN extents: one column (still exact)
+      if (!(invy < 1e30f)) invy = 0.f;
+    }
+    // boxes large against the segment extent (< 8 mean boxes per side): every candidate overlaps
+    // a large share of the kept list, and the 16-way split of the whole list is faster
+    if (gx * gy < 256) grid = false;
     // the next block's candidates are fetched one iteration ahead (their load latency overlaps
     // this block's tests); compaction only writes slots < blk + 64, so the prefetch is safe
     float4 cb_nx = lane < n ? boxes[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
@@ -486,8 +572,29 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
         cid_nx = idx[blk + 64 + lane];
       }
       const int nk = s_nk;
+      const bool use_grid = grid && !s_ovf;
+      const bool cvalid = cb.z > cb.x && cb.w > cb.y;
+      int x0 = 0, y0 = 0, nx = 1, ncell = 0;
+      if (use_grid) {
+        x0 = nms_cell(cb.x, ox, invx, gx);
+        y0 = nms_cell(cb.y, oy, invy, gy);
+        nx = nms_cell(cb.z, ox, invx, gx) - x0 + 1;
+        ncell = nx * (nms_cell(cb.w, oy, invy, gy) - y0 + 1);
+      }
       bool sup = false;
-      if (has) {
+      if (has && use_grid) {
+        if (cvalid) {
+          // slot ncell = the wide-box list; slots [0, ncell) the covered cells, split over waves
+          for (int q = wave; q <= ncell && !sup; q += 16) {
+            const int h = q == ncell ? NMS_GMAX * NMS_GMAX : (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
+            for (int e = s_head[h]; e >= 0;) {
+              const int2 lk = s_link[e];
+              if (iou_gt_f(s_kept[lk.x], cb, thr_f, false)) { sup = true; break; }
+              e = lk.y;
+            }
+          }
+        }
+      } else if (has) {
         const int nl = min(nk, NMS_KEPT_LDS);
         int k = wave;
         for (; k + 48 < nl; k += 64) {        // 4 independent LDS reads in flight
@@ -526,6 +633,20 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
           boxes[pos] = cb;
           idx[pos] = cid;
           if (pos < NMS_KEPT_LDS) s_kept[pos] = cb;
+          if (use_grid && cvalid) {
+            const int cnt_l = ncell > 64 ? 1 : ncell;      // > 64 cells: the wide-box list
+            const int base = pos < NMS_KEPT_LDS ? atomicAdd(&s_nlink, cnt_l) : NMS_LINKS;
+            if (base + cnt_l > NMS_LINKS) {
+              s_ovf = 1;        // the remaining blocks test the whole kept list
+            } else if (ncell > 64) {
+              s_link[base] = make_int2(pos, atomicExch(&s_head[NMS_GMAX * NMS_GMAX], base));
+            } else {
+              for (int q = 0; q < ncell; ++q) {
+                const int h = (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
+                s_link[base + q] = make_int2(pos, atomicExch(&s_head[h], base + q));
+              }
+            }
+          }
         }
         if (lane == 0) s_nk = nk + __popcll(am);
       }
@@ -649,7 +770,7 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     if (hipFuncSetAttribute((const void*)nms_big_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             NMS_BIG_LDS_KEYS * 8) != hipSuccess ||
         hipFuncSetAttribute((const void*)nms_big_greedy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            NMS_KEPT_LDS * 16) != hipSuccess)
+                            (int)NMS_GREEDY_LDS) != hipSuccess)
       return YMS_ERR_LAUNCH;
     attr_set = true;
   }
@@ -661,7 +782,7 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     const unsigned segs = (unsigned)std::min(256, n * nc);
     hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_BIG_LDS_KEYS * 8, st, A, nc,
                        boxes_xyxy, w);
-    hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), (size_t)NMS_KEPT_LDS * 16, st, A, nc,
+    hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
                        thr_f, full, w);
   }
   yms_status e = launch_status();
