@@ -13,6 +13,7 @@
 //           one wave.  IoU arithmetic is torchvision's CPU kernel op-for-op (fp32, no +1,
 //           ratio compared as double), FP contraction disabled, so keep indices are
 //           bit-exact against the CPU oracle on identical decoded inputs.
+#include <cstdlib>
 #include "yms_common.hpp"
 
 #pragma clang fp contract(off)
@@ -492,11 +493,13 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
+__global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, int grid_min_kept,
+                                                              NmsWs ws) {
   extern __shared__ float4 s_kept[];                              // [NMS_KEPT_LDS]
   int2* s_link = reinterpret_cast<int2*>(s_kept + NMS_KEPT_LDS);  // [NMS_LINKS] (kept idx, next)
   int* s_head = reinterpret_cast<int*>(s_link + NMS_LINKS);       // [NMS_GMAX^2 + 1]
   __shared__ unsigned long long s_sup[16];
+  __shared__ int s_base[64], s_pos[64];
   __shared__ float s_red[7][16];
   __shared__ int s_nk, s_nlink, s_ovf;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -582,7 +585,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
         ncell = nx * (nms_cell(cb.w, oy, invy, gy) - y0 + 1);
       }
       bool sup = false;
-      if (has && use_grid) {
+      if (has && use_grid && nk >= grid_min_kept) {
         if (cvalid) {
           // slot ncell = the wide-box list; slots [0, ncell) the covered cells, split over waves
           for (int q = wave; q <= ncell && !sup; q += 16) {
@@ -629,28 +632,40 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
           am = __ballot(alive);
         }
         const int pos = nk + __popcll(am & ((1ull << lane) - 1ull));
+        int base = -1;
         if (alive) {          // pos <= blk + lane: only already-consumed slots are overwritten
           boxes[pos] = cb;
           idx[pos] = cid;
           if (pos < NMS_KEPT_LDS) s_kept[pos] = cb;
           if (use_grid && cvalid) {
             const int cnt_l = ncell > 64 ? 1 : ncell;      // > 64 cells: the wide-box list
-            const int base = pos < NMS_KEPT_LDS ? atomicAdd(&s_nlink, cnt_l) : NMS_LINKS;
+            base = pos < NMS_KEPT_LDS ? atomicAdd(&s_nlink, cnt_l) : NMS_LINKS;
             if (base + cnt_l > NMS_LINKS) {
-              s_ovf = 1;        // the remaining blocks test the whole kept list
-            } else if (ncell > 64) {
-              s_link[base] = make_int2(pos, atomicExch(&s_head[NMS_GMAX * NMS_GMAX], base));
-            } else {
-              for (int q = 0; q < ncell; ++q) {
-                const int h = (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
-                s_link[base + q] = make_int2(pos, atomicExch(&s_head[h], base + q));
-              }
+              s_ovf = 1;      // the remaining blocks test the whole kept list
+              base = -1;
             }
           }
         }
+        s_base[lane] = base;
+        s_pos[lane] = pos;
         if (lane == 0) s_nk = nk + __popcll(am);
       }
       __syncthreads();
+      if (use_grid) {       // block-uniform: link the new kept boxes, cells split over the waves
+        const int base = s_base[lane];
+        if (base >= 0) {
+          const int pos = s_pos[lane];
+          if (ncell > 64) {
+            if (wave == 0) s_link[base] = make_int2(pos, atomicExch(&s_head[NMS_GMAX * NMS_GMAX], base));
+          } else {
+            for (int q = wave; q < ncell; q += 16) {
+              const int h = (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
+              s_link[base + q] = make_int2(pos, atomicExch(&s_head[h], base + q));
+            }
+          }
+        }
+        __syncthreads();
+      }
     }
     if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
     __syncthreads();
@@ -782,8 +797,14 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     const unsigned segs = (unsigned)std::min(256, n * nc);
     hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_BIG_LDS_KEYS * 8, st, A, nc,
                        boxes_xyxy, w);
+    // grid lookups from this many kept boxes on (below, the 16-way split of the whole kept list
+    // is as fast); YMS_NMS_GRID_MIN_KEPT overrides it for A/B measurements
+    static const int grid_min = [] {
+      const char* e = getenv("YMS_NMS_GRID_MIN_KEPT");
+      return e ? atoi(e) : 128;
+    }();
     hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
-                       thr_f, full, w);
+                       thr_f, full, grid_min, w);
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
