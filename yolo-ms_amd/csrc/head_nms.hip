@@ -298,12 +298,12 @@ __global__ __launch_bounds__(256) void nms_class_kernel(int A, int nc, const flo
 }
 
 // Large segments (> NMS_CAP boxes: nc=1, or one dominant class of a random-init model).
-//  nms_big_sort : one 1024-thread block per segment, bitonic sort (LDS when <= 16K keys),
+//  nms_big_sort : one 1024-thread block per segment: register bitonic sort8192 up to 8192 keys,
+//                 above that merge-path rounds over chunks sorted by nms_chunk_sort_kernel;
 //                 sorted boxes + anchor ids to global.
 //  nms_big_greedy: kept-list greedy suppression (below).  Disjoint boxes take an early exit
 //                 (ovr = 0, or 0/0 = NaN, is never > thr for thr >= 0); the ratio compare uses
 //                 the float threshold exactly equivalent to torchvision's double compare.
-constexpr int NMS_BIG_LDS_KEYS = 16384;
 
 __device__ __forceinline__ bool iou_gt_f(const float4& i, const float4& j, float thr_f, bool full) {
   const float xx1 = fmaxf(i.x, j.x);
@@ -405,6 +405,52 @@ __device__ void sort8192(uint64_t* keys, int n) {
   __syncthreads();
 }
 
+// Segments of more than 8192 keys: 8192-key chunks are sorted by sort8192 in parallel blocks
+// (nms_chunk_sort_kernel, one block per (segment, chunk)), then nms_big_sort_kernel merges the
+// sorted runs pairwise by merge path (each of the 1024 threads finds its split of the output
+// diagonal by binary search and merges its share sequentially), ping-ponging between the
+// segment's key slots and its box slots (16 B per key, so 8 B per key of scratch is free until
+// the boxes are written).  Keys are unique (anchor id in the low word), so the order is total.
+constexpr int NMS_CHUNK = 8192;
+
+__global__ __launch_bounds__(1024) void nms_chunk_sort_kernel(int A, int nc, NmsWs ws) {
+  extern __shared__ uint64_t s_big[];
+  const int nch = (A + NMS_CHUNK - 1) / NMS_CHUNK;
+  const int nbig = ws.big[0];
+  for (int it = blockIdx.x; it < nbig * nch; it += gridDim.x) {
+    const int sg = it / nch, ch = it % nch;
+    const int b = ws.big[1 + 2 * sg], c = ws.big[2 + 2 * sg];
+    const int n = ws.cls_cnt[(long)b * nc + c];
+    if (n <= NMS_CHUNK || ch * NMS_CHUNK >= n) continue;    // block-uniform
+    uint64_t* gk = ws.gkeys + (long)b * A + ws.cls_off[(long)b * nc + c] + (long)ch * NMS_CHUNK;
+    const int len = min(NMS_CHUNK, n - ch * NMS_CHUNK);
+    for (int i = threadIdx.x; i < len; i += 1024) s_big[i] = gk[i];
+    __syncthreads();
+    sort8192(s_big, len);     // ends with a barrier
+    for (int i = threadIdx.x; i < len; i += 1024) gk[i] = s_big[i];
+    __syncthreads();
+  }
+}
+
+// merge sorted runs x[0, la) and y[0, lb) into out[0, la + lb) with 1024 threads
+__device__ void merge_path_1024(const uint64_t* x, int la, const uint64_t* y, int lb, uint64_t* out) {
+  const int len = la + lb, t = threadIdx.x;
+  const int d0 = (int)((long)len * t / 1024), d1 = (int)((long)len * (t + 1) / 1024);
+  if (d0 >= d1) return;
+  int lo = max(0, d0 - lb), hi = min(d0, la);
+  while (lo < hi) {            // smallest i with x[i] > y[d0 - i - 1]
+    const int mid = (lo + hi) >> 1;
+    if (x[mid] < y[d0 - mid - 1]) lo = mid + 1; else hi = mid;
+  }
+  int i = lo, j = d0 - lo;
+  uint64_t xv = i < la ? x[i] : ~0ull, yv = j < lb ? y[j] : ~0ull;
+  for (int d = d0; d < d1; ++d) {
+    const bool tx = j >= lb || (i < la && xv < yv);
+    out[d] = tx ? xv : yv;
+    if (tx) { ++i; xv = i < la ? x[i] : ~0ull; } else { ++j; yv = j < lb ? y[j] : ~0ull; }
+  }
+}
+
 __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const float* bxy, NmsWs ws) {
   extern __shared__ uint64_t s_big[];
   const int tid = threadIdx.x;
@@ -414,30 +460,34 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
     const int n = ws.cls_cnt[(long)b * nc + c];
     const int off = ws.cls_off[(long)b * nc + c];
     uint64_t* gk = ws.gkeys + (long)b * A + off;
-    const bool inlds = n <= NMS_BIG_LDS_KEYS;
-    uint64_t* keys = inlds ? s_big : gk;
-    if (n <= 8192) {
+    uint64_t* tmp = reinterpret_cast<uint64_t*>(ws.gboxes + (long)b * A + off);   // 2n keys of room
+    const uint64_t* keys;
+    if (n <= NMS_CHUNK) {
       for (int i = tid; i < n; i += 1024) s_big[i] = gk[i];
       __syncthreads();
       sort8192(s_big, n);
+      keys = s_big;
     } else {
-    if (inlds)
-      for (int i = tid; i < n; i += 1024) s_big[i] = gk[i];
-    __syncthreads();
-    int N2 = 1;
-    while (N2 < n) N2 <<= 1;
-    for (int k = 2; k <= N2; k <<= 1) {
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int t = tid; t < N2; t += 1024) {
-          const int partner = (j == (k >> 1)) ? (t ^ (k - 1)) : (t ^ j);
-          if (partner > t && partner < n) {
-            const uint64_t x = keys[t], y = keys[partner];
-            if (y < x) { keys[t] = y; keys[partner] = x; }
-          }
+      // runs of NMS_CHUNK sorted by nms_chunk_sort_kernel; the last round must land in gk (the
+      // box writes below overwrite tmp), so an odd round count starts from a copy in tmp
+      int rounds = 0;
+      for (int L = NMS_CHUNK; L < n; L <<= 1) ++rounds;
+      uint64_t* src = gk;
+      uint64_t* dst = tmp;
+      if (rounds & 1) {
+        for (int i = tid; i < n; i += 1024) tmp[i] = gk[i];
+        src = tmp; dst = gk;
+      }
+      __syncthreads();
+      for (int L = NMS_CHUNK; L < n; L <<= 1) {
+        for (int lo = 0; lo < n; lo += 2 * L) {
+          const int la = min(L, n - lo), lb = max(0, min(L, n - lo - L));
+          merge_path_1024(src + lo, la, src + lo + la, lb, dst + lo);
         }
         __syncthreads();
+        uint64_t* t = src; src = dst; dst = t;
       }
-    }
+      keys = src;           // == gk
     }
     float4* boxes = ws.gboxes + (long)b * A + off;
     const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
@@ -783,7 +833,9 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
   static bool attr_set = false;
   if (!attr_set) {
     if (hipFuncSetAttribute((const void*)nms_big_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            NMS_BIG_LDS_KEYS * 8) != hipSuccess ||
+                            NMS_CHUNK * 8) != hipSuccess ||
+        hipFuncSetAttribute((const void*)nms_chunk_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NMS_CHUNK * 8) != hipSuccess ||
         hipFuncSetAttribute((const void*)nms_big_greedy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)NMS_GREEDY_LDS) != hipSuccess)
       return YMS_ERR_LAUNCH;
@@ -795,7 +847,9 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     if ((double)thr_f > iou) thr_f = nextafterf(thr_f, -INFINITY);
     const int full = iou < 0.0 ? 1 : 0;
     const unsigned segs = (unsigned)std::min(256, n * nc);
-    hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_BIG_LDS_KEYS * 8, st, A, nc,
+    if (A > NMS_CHUNK)
+      hipLaunchKernelGGL(nms_chunk_sort_kernel, dim3(256), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc, w);
+    hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc,
                        boxes_xyxy, w);
     // grid lookups from this many kept boxes on (below, the 16-way split of the whole kept list
     // is as fast); YMS_NMS_GRID_MIN_KEPT overrides it for A/B measurements
