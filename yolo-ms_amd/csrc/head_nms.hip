@@ -505,21 +505,31 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
 // are taken in 64-blocks; all 16 waves test the block against the boxes kept so far, then wave 0
 // resolves the block itself in score order, visiting only the still-alive candidates.
 //
-// Kept boxes are bucketed on a per-segment Gx x Gy grid (cell ~ the mean box size): a kept box is
-// linked into every cell its [x1,x2] x [y1,y2] range maps to, and a candidate tests only the
-// lists of the cells its own range maps to (plus a list of boxes spanning > 64 cells).  Exact: a
+// Kept boxes are bucketed on a per-segment Gx x Gy grid (cell ~ half the mean box size): a kept
+// box is appended to every cell its [x1,x2] x [y1,y2] range maps to (fixed-capacity per-cell
+// arrays of kept indices, read 4 at a time), and a candidate tests only the arrays of the cells
+// its own range maps to (plus a list of boxes spanning > 64 cells).  Exact: a
 // positive intersection has a = max(x1_i, x1_j) inside both x-ranges, and the cell map
 // f(v) = clamp(floor((v - ox) * inv)) is monotone in v, so f(a) lies in both cell ranges (same
 // for y); a is an input coordinate, so no rounding enters the argument.  Zero-area and inverted
 // boxes never take part in a positive intersection (iou_gt_f returns false), so they are not
 // linked and are never tested.  The segment falls back to testing the whole kept list (the
 // pre-grid algorithm) for a negative threshold (`full`), a non-finite coordinate, or once the
-// LDS kept mirror / link pool is full.
+// LDS kept mirror or a cell array is full.
 constexpr int NMS_KEPT_LDS = 4096;   // kept boxes mirrored in LDS (64 KB); beyond: global
-constexpr int NMS_LINKS = 10240;     // (kept index, next) link pool (80 KB)
+constexpr int NMS_CELL_CAP = 32;     // kept indices per cell (uint16)
 constexpr int NMS_GMAX = 32;         // grid side cap; head slot NMS_GMAX^2 = the wide-box list
+constexpr int NMS_CELLS = NMS_GMAX * NMS_GMAX + 1;
 constexpr size_t NMS_GREEDY_LDS =
-    (size_t)NMS_KEPT_LDS * 16 + (size_t)NMS_LINKS * 8 + (size_t)(NMS_GMAX * NMS_GMAX + 1) * 4;
+    (size_t)NMS_KEPT_LDS * 16 + (size_t)NMS_CELLS * NMS_CELL_CAP * 2 + (size_t)NMS_CELLS * 4;
+
+// Barrier ordering LDS only: outstanding global loads (the next block's candidate prefetch) and
+// stores (kept-list compaction) stay in flight across it, unlike __syncthreads()'s vmcnt(0).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
 
 __device__ __forceinline__ int nms_cell(float v, float o, float inv, int g) {
   float f = (v - o) * inv;
@@ -546,12 +556,12 @@ __device__ __forceinline__ float wave_sum(float v) {
 __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, int grid_min_kept,
                                                               NmsWs ws) {
   extern __shared__ float4 s_kept[];                              // [NMS_KEPT_LDS]
-  int2* s_link = reinterpret_cast<int2*>(s_kept + NMS_KEPT_LDS);  // [NMS_LINKS] (kept idx, next)
-  int* s_head = reinterpret_cast<int*>(s_link + NMS_LINKS);       // [NMS_GMAX^2 + 1]
+  uint16_t* s_cell = reinterpret_cast<uint16_t*>(s_kept + NMS_KEPT_LDS);   // [NMS_CELLS][CAP]
+  int* s_ccnt = reinterpret_cast<int*>(s_cell + NMS_CELLS * NMS_CELL_CAP);  // [NMS_CELLS]
   __shared__ unsigned long long s_sup[16];
   __shared__ int s_base[64], s_pos[64];
   __shared__ float s_red[7][16];
-  __shared__ int s_nk, s_nlink, s_ovf;
+  __shared__ int s_nk, s_ovf;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbig = ws.big[0];
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
@@ -583,8 +593,8 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
         if (wbad) s_red[6][wave] = -1.f;
       }
     }
-    for (int i = tid; i <= NMS_GMAX * NMS_GMAX; i += 1024) s_head[i] = -1;
-    if (tid == 0) { s_nk = 0; s_nlink = 0; s_ovf = 0; }
+    for (int i = tid; i < NMS_CELLS; i += 1024) s_ccnt[i] = 0;
+    if (tid == 0) { s_nk = 0; s_ovf = 0; }
     __syncthreads();
     float ox = INFINITY, oy = INFINITY, ex = -INFINITY, ey = -INFINITY, sw = 0.f, sh = 0.f, cnt = 0.f;
     bool bad = false;
@@ -640,10 +650,14 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
           // slot ncell = the wide-box list; slots [0, ncell) the covered cells, split over waves
           for (int q = wave; q <= ncell && !sup; q += 16) {
             const int h = q == ncell ? NMS_GMAX * NMS_GMAX : (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
-            for (int e = s_head[h]; e >= 0;) {
-              const int2 lk = s_link[e];
-              if (iou_gt_f(s_kept[lk.x], cb, thr_f, false)) { sup = true; break; }
-              e = lk.y;
+            const int cn = min(s_ccnt[h], NMS_CELL_CAP);
+            const uint16_t* cl = s_cell + h * NMS_CELL_CAP;
+            for (int k = 0; k < cn; k += 4) {     // 4 independent index / box reads in flight
+              const int e0 = cl[k], e1 = k + 1 < cn ? cl[k + 1] : e0;
+              const int e2 = k + 2 < cn ? cl[k + 2] : e0, e3 = k + 3 < cn ? cl[k + 3] : e0;
+              const float4 k0 = s_kept[e0], k1 = s_kept[e1], k2 = s_kept[e2], k3 = s_kept[e3];
+              if (iou_gt_f(k0, cb, thr_f, false) || iou_gt_f(k1, cb, thr_f, false) ||
+                  iou_gt_f(k2, cb, thr_f, false) || iou_gt_f(k3, cb, thr_f, false)) { sup = true; break; }
             }
           }
         }
@@ -661,7 +675,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
       }
       const unsigned long long sm = __ballot(sup);
       if (lane == 0) s_sup[wave] = sm;
-      __syncthreads();
+      lds_barrier();
       if (wave == 0) {
         unsigned long long allsup = 0;
 #pragma unroll
@@ -682,39 +696,35 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
           am = __ballot(alive);
         }
         const int pos = nk + __popcll(am & ((1ull << lane) - 1ull));
-        int base = -1;
+        bool link = false;
         if (alive) {          // pos <= blk + lane: only already-consumed slots are overwritten
           boxes[pos] = cb;
           idx[pos] = cid;
           if (pos < NMS_KEPT_LDS) s_kept[pos] = cb;
           if (use_grid && cvalid) {
-            const int cnt_l = ncell > 64 ? 1 : ncell;      // > 64 cells: the wide-box list
-            base = pos < NMS_KEPT_LDS ? atomicAdd(&s_nlink, cnt_l) : NMS_LINKS;
-            if (base + cnt_l > NMS_LINKS) {
-              s_ovf = 1;      // the remaining blocks test the whole kept list
-              base = -1;
-            }
+            if (pos < NMS_KEPT_LDS) link = true;
+            else s_ovf = 1;   // the remaining blocks test the whole kept list
           }
         }
-        s_base[lane] = base;
+        s_base[lane] = link ? 1 : 0;
         s_pos[lane] = pos;
         if (lane == 0) s_nk = nk + __popcll(am);
       }
-      __syncthreads();
+      // kept boxes past the LDS mirror are read back from global by the fallback path: only then
+      // do the global stores above need the full barrier
+      if (nk + 64 > NMS_KEPT_LDS) __syncthreads(); else lds_barrier();
       if (use_grid) {       // block-uniform: link the new kept boxes, cells split over the waves
-        const int base = s_base[lane];
-        if (base >= 0) {
+        if (s_base[lane]) {
           const int pos = s_pos[lane];
-          if (ncell > 64) {
-            if (wave == 0) s_link[base] = make_int2(pos, atomicExch(&s_head[NMS_GMAX * NMS_GMAX], base));
-          } else {
-            for (int q = wave; q < ncell; q += 16) {
-              const int h = (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
-              s_link[base + q] = make_int2(pos, atomicExch(&s_head[h], base + q));
-            }
+          const int nq = ncell > 64 ? 1 : ncell;           // > 64 cells: the wide-box list
+          for (int q = wave; q < nq; q += 16) {
+            const int h = ncell > 64 ? NMS_GMAX * NMS_GMAX : (y0 + q / nx) * NMS_GMAX + x0 + q % nx;
+            const int slot = atomicAdd(&s_ccnt[h], 1);
+            if (slot < NMS_CELL_CAP) s_cell[h * NMS_CELL_CAP + slot] = (uint16_t)pos;
+            else s_ovf = 1;   // full cell: the remaining blocks test the whole kept list
           }
         }
-        __syncthreads();
+        lds_barrier();
       }
     }
     if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
