@@ -258,12 +258,14 @@ def main():
         line = {"metric": "images/sec (train+infer) YOLO-MS-S 640x640 bf16 at 1/2/4/8 MI355X; mAP parity",
                 "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-                "data": "synthetic (randn images, torch-default random-init weights of the YOLOv8-s graph)"}
+                "data": f"synthetic (randn images, torch-default random-init weights of the YOLOv8-{a.version} graph)"}
         if "train" in result:
             tr = result["train"]
             line["value"] = round(tr["img_s"], 2)
             line["ms_per_step"] = round(tr["dt"] / a.steps * 1e3, 3)
-            line["config"] = {"workload": f"configs[2]: YOLO-MS-S (reference YOLOv8-'{a.version}' graph) "
+            tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L"}.get(
+                a.version, f"custom: YOLO-MS-{a.version.upper()}")
+            line["config"] = {"workload": f"{tcfg} (reference YOLOv8-'{a.version}' graph) "
                                           f"{a.size}x{a.size} {a.dtype} training, B={a.batch}/GPU, fwd+loss+bwd+"
                                           "allreduce+SGD-nesterov step",
                               "global_batch": a.batch * world, "per_gpu_batch": a.batch, "img": a.size,
@@ -277,9 +279,12 @@ def main():
                                                  f"({a.dtype} MFMA), one training step")
                 add_traffic(line["roofline"], "train", line["config"]["workload"])
         if "infer" in result:
+            icfg = {(640, "bf16"): "configs[1]", (1280, "f16"): "configs[4]"}.get((a.size, a.dtype), "custom")
+            if a.version != "s":
+                icfg += f" (YOLO-MS-{a.version.upper()} graph)"
             inf = {"value": round(result["infer"]["img_s"], 2), "unit": "images/sec",
                    "ms_per_batch": round(result["infer"]["dt"] / a.steps * 1e3, 3),
-                   "workload": f"configs[1]: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU "
+                   "workload": f"{icfg}: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU "
                                "(forward + decode + class-wise NMS)"}
             if "infer_prof" in result:
                 inf["roofline"] = conv_roofline(result["infer_prof"], f"conv implicit-GEMM fwd ({a.dtype} MFMA)")
