@@ -625,6 +625,15 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
     // this block's tests); compaction only writes slots < blk + 64, so the prefetch is safe
     float4 cb_nx = lane < n ? boxes[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
     int cid_nx = lane < n ? idx[lane] : 0;
+#ifdef YMS_NMS_PROF
+    // dev instrumentation (make -C yolo-ms_amd/csrc nmsprof; tools/nms_prof_run.py): wave 0's
+    // cycles per step phase, printed for the segments of image 0
+    long long pacc[6] = {0, 0, 0, 0, 0, 0}, pt = clock64();
+    int nres = 0;
+#define PMARK(k) do { if (tid == 0) { const long long q_ = clock64(); pacc[k] += q_ - pt; pt = q_; } } while (0)
+#else
+#define PMARK(k) do {} while (0)
+#endif
     for (int blk = 0; blk < n; blk += 64) {
       const int m = min(64, n - blk);
       const bool has = lane < m;
@@ -675,7 +684,9 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
       }
       const unsigned long long sm = __ballot(sup);
       if (lane == 0) s_sup[wave] = sm;
+      PMARK(0);
       lds_barrier();
+      PMARK(1);
       if (wave == 0) {
         unsigned long long allsup = 0;
 #pragma unroll
@@ -695,6 +706,10 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
           if (alive && lane > i && iou_gt_f(bi, cb, thr_f, full)) alive = false;
           am = __ballot(alive);
         }
+        PMARK(2);
+#ifdef YMS_NMS_PROF
+        nres += __popcll(done);
+#endif
         const int pos = nk + __popcll(am & ((1ull << lane) - 1ull));
         bool link = false;
         if (alive) {          // pos <= blk + lane: only already-consumed slots are overwritten
@@ -712,7 +727,9 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
       }
       // kept boxes past the LDS mirror are read back from global by the fallback path: only then
       // do the global stores above need the full barrier
+      PMARK(3);
       if (nk + 64 > NMS_KEPT_LDS) __syncthreads(); else lds_barrier();
+      PMARK(4);
       if (use_grid) {       // block-uniform: link the new kept boxes, cells split over the waves
         if (s_base[lane]) {
           const int pos = s_pos[lane];
@@ -726,7 +743,15 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
         }
         lds_barrier();
       }
+      PMARK(5);
     }
+#ifdef YMS_NMS_PROF
+    if (tid == 0 && b == 0)
+      printf("NMSPROF seg n=%d kept=%d grid=%d gx=%d gy=%d ovf=%d resolved=%d test=%lld bar1=%lld "
+             "resolve=%lld write=%lld bar2=%lld insert=%lld\n", n, s_nk, (int)grid, gx, gy, s_ovf, nres,
+             pacc[0], pacc[1], pacc[2], pacc[3], pacc[4], pacc[5]);
+#endif
+#undef PMARK
     if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
     __syncthreads();
   }
