@@ -8,6 +8,7 @@
 //   Bottleneck residual (always on)                     yolov8/model/components.py:87-93
 //   SPPF: three chained MaxPool2d(5, 1, 2) + cat        yolov8/model/components.py:136-146
 //   Upsample nearest x2                                 yolov8/model/components.py:159-160
+#include <cstdlib>
 #include <algorithm>
 
 #include "yms_common.hpp"
@@ -269,22 +270,26 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
   }
 }
 
-__global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long count,
-                                                               float* dgamma, float* dbeta, float* coef) {
-  __shared__ double red[2][32][33];
+// 32 channels x TY row lanes per block.  TY = 8 (256 threads) by default: with the weight
+// gradients running on the side stream, a 1024-thread block waits for a whole CU to drain,
+// which puts that wait on the main stream's critical path.
+template <int TY>
+__global__ __launch_bounds__(32 * TY) void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long count,
+                                                                  float* dgamma, float* dbeta, float* coef) {
+  __shared__ double red[2][TY][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int ch = blockIdx.x * 32 + tx;
   double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
   if (ch < c) {
     int r = ty;
-    for (; r + 96 < rows; r += 128) {
+    for (; r + 3 * TY < rows; r += 4 * TY) {
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
-        a1[u] += ws[(long)(r + 32 * u) * 2 * c + ch];
-        a2[u] += ws[(long)(r + 32 * u) * 2 * c + c + ch];
+        a1[u] += ws[(long)(r + TY * u) * 2 * c + ch];
+        a2[u] += ws[(long)(r + TY * u) * 2 * c + c + ch];
       }
     }
-    for (; r < rows; r += 32) {
+    for (; r < rows; r += TY) {
       a1[0] += ws[(long)r * 2 * c + ch];
       a2[0] += ws[(long)r * 2 * c + c + ch];
     }
@@ -294,7 +299,7 @@ __global__ __launch_bounds__(1024) void bn_bwd_finalize_kernel(int c, const floa
   __syncthreads();
   if (ty == 0 && ch < c) {
     double t1 = 0.0, t2 = 0.0;
-    for (int k = 0; k < 32; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
+    for (int k = 0; k < TY; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
     if (dbeta) dbeta[ch] = (float)t1;
     if (dgamma) dgamma[ch] = (float)t2;
     if (coef) {
@@ -722,8 +727,13 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
 yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count, float* dgamma,
                                    float* dbeta, float* coef, void* stream) {
   if (c <= 0 || !ws || rows <= 0 || count <= 0) return YMS_ERR_INVALID;
-  hipLaunchKernelGGL(bn_bwd_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, ws,
-                     rows, count, dgamma, dbeta, coef);
+  static const int wide = getenv("YMS_BN_FIN_1024") ? atoi(getenv("YMS_BN_FIN_1024")) : 0;   // dev A/B
+  if (wide)
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, ws,
+                       rows, count, dgamma, dbeta, coef);
+  else
+    hipLaunchKernelGGL(bn_bwd_finalize_kernel<8>, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, ws,
+                       rows, count, dgamma, dbeta, coef);
   return launch_status();
 }
 
