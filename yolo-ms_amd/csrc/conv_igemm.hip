@@ -1298,24 +1298,31 @@ template <typename T, int KS, int MODE, int EPI, bool UNI>
 static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st) {
   NTParams p = p0;
   static const int variant = getenv("YMS_NT_VARIANT") ? atoi(getenv("YMS_NT_VARIANT")) : 0;
+  // dgrad grids: one block per output tile by default.  The weight gradients run beside dgrad on
+  // the side stream, and persistent blocks that start late on CUs the wgrad kernels hold would
+  // each still owe their fixed share of tiles (interleaved A/B: 19.91 -> 19.74 ms/step).
+  // YMS_NT_DGRAD_MULT = m launches OCC x CUs x m persistent blocks instead (dev A/B; m = 1 is
+  // the persistent grid).
+  static const int dmult = getenv("YMS_NT_DGRAD_MULT") ? std::max(1, atoi(getenv("YMS_NT_DGRAD_MULT"))) : 1 << 16;
+  const int mult = MODE == MODE_FWD ? 1 : dmult;
   // 8-wave blocks at 2-3 per CU (4-6 waves per SIMD) hide the ds_read -> MFMA and barrier
   // latencies that 4-wave blocks expose; variant 6 (dev A/B): 256-row tiles of 16 waves at
   // 1 block per CU (25% fewer LDS-fill bytes per FLOP, 2 k-tiles in flight).
   if (cfg == 0) {
     p.tiles_n = cdiv(p.Ncols, 128);
     if (variant == 6)
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1>, p, 256, gy, st, 1, 1024);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1>, p, 256, gy, st, 1 * mult, 1024);
     else
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, 2, 512);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, 2 * mult, 512);
   } else if (cfg == 1) {
     p.tiles_n = cdiv(p.Ncols, 64);
     if (variant == 6)
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 64, 8, 2, 3, UNI, 1>, p, 256, gy, st, 1, 1024);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 64, 8, 2, 3, UNI, 1>, p, 256, gy, st, 1 * mult, 1024);
     else
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, 3, 512);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, 3 * mult, 512);
   } else {
     p.tiles_n = cdiv(p.Ncols, 32);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, 2, 512);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, 2 * mult, 512);
   }
 }
 
