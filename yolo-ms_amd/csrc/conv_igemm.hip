@@ -1304,7 +1304,8 @@ static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st)
   // YMS_NT_DGRAD_MULT = m launches OCC x CUs x m persistent blocks instead (dev A/B; m = 1 is
   // the persistent grid).
   static const int dmult = getenv("YMS_NT_DGRAD_MULT") ? std::max(1, atoi(getenv("YMS_NT_DGRAD_MULT"))) : 1 << 16;
-  const int mult = MODE == MODE_FWD ? 1 : dmult;
+  static const int fmult = getenv("YMS_NT_FWD_MULT") ? std::max(1, atoi(getenv("YMS_NT_FWD_MULT"))) : 1;
+  const int mult = MODE == MODE_FWD ? fmult : dmult;
   // 8-wave blocks at 2-3 per CU (4-6 waves per SIMD) hide the ds_read -> MFMA and barrier
   // latencies that 4-wave blocks expose; variant 6 (dev A/B): 256-row tiles of 16 waves at
   // 1 block per CU (25% fewer LDS-fill bytes per FLOP, 2 k-tiles in flight).
