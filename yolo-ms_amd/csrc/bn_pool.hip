@@ -691,8 +691,12 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
 
 int yms_bn_bwd_rows(long npix) {
   if (npix <= 0) return 0;
+  // partial-sum rows = reduce blocks, at most 512: 2 blocks per CU leave room for the
+  // side-stream wgrad and halve the finalize's table (interleaved A/B of the training step:
+  // cap 1024 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms; YMS_BN_BWD_ROWS_CAP overrides)
+  static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 512;
   long rows = (npix + 63) / 64;
-  if (rows > 1024) rows = 1024;
+  if (rows > cap) rows = cap;
   return (int)rows;
 }
 
