@@ -667,9 +667,9 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
 // pixels per block for the channel-stationary kernels: about four U-pixel iterations per
 // thread (amortises the per-channel parameter loads; measured best of 1/2/4/8), at most 8192
 // blocks
-static long elem_ppb(long npix, int c) {
+static long elem_ppb(long npix, int c, int iters = 4) {
   const long py = 256 / ((c + 7) / 8);
-  const long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * 4), 1), 8192);
+  const long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * iters), 1), 8192);
   return (npix + blocks - 1) / blocks;
 }
 
@@ -750,7 +750,8 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
   if (!vok(z_ld, z_off, c) || !vok(gy_ld, gy_off, c) || !vok(dz_ld, dz_off, c)) return YMS_ERR_INVALID;
   if (gres && !vok(gres_ld, gres_off, c)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = elem_ppb(npix, c);
+  static const int iters = getenv("YMS_BN_APPLY_ITERS") ? std::max(1, atoi(getenv("YMS_BN_APPLY_ITERS"))) : 4;
+  const long ppb = elem_ppb(npix, c, iters);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
   YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
