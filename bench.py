@@ -33,8 +33,8 @@ def log(*a):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=100)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--batch", type=int, default=64, help="training images per GPU (configs[2])")
     ap.add_argument("--infer-batch", type=int, default=32, help="inference batch (configs[1])")
     ap.add_argument("--size", type=int, default=640)
@@ -49,25 +49,33 @@ def parse():
 
 
 def timed(fn, steps, warmup, world):
+    """W untimed warmups, then exactly K steps bracketed by barrier + synchronize on both sides
+    (max over ranks).  Also returns the median per-step GPU time from events recorded between
+    steps on the compute stream (no host sync inside the timed loop)."""
     for _ in range(warmup):
         fn()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(steps + 1)]
     t0 = time.perf_counter()
+    ev[0].record()
     for i in range(steps):
         fn()
+        ev[i + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    per = sorted(ev[i].elapsed_time(ev[i + 1]) for i in range(steps))
+    med = per[len(per) // 2] if per else 0.0
     if world > 1:
-        t = torch.tensor([dt], device="cuda", dtype=torch.float64)
+        t = torch.tensor([dt, med], device="cuda", dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        dt = t.item()
-    return dt
+        dt, med = t[0].item(), t[1].item()
+    return dt, med
 
 
 def add_traffic(roof, mode, workload):
@@ -124,9 +132,18 @@ def pmc_traffic(mode, workload):
     return None, None, None
 
 
-def cpu_baseline_train(version, nc, size, batch=4, steps=4):
+def cpu_threads():
+    """Host threads for the CPU baseline: the box's CPU share for one GPU (OMP_NUM_THREADS, which
+    the GPU pool sets to 16 -- os.cpu_count() there reports the whole machine), else all cores."""
+    n = int(os.environ.get("OMP_NUM_THREADS") or 0) or os.cpu_count() or 1
+    torch.set_num_threads(n)
+    return n
+
+
+def cpu_baseline_train(version, nc, size, batch=8, steps=8):
     """Oracle (fp32 torch-CPU restatement of the reference graph) train step on host cores."""
     from oracle import model_ref as M
+    threads = cpu_threads()
     sd = M.init_params(version, nc)
     p = {k: (t.clone().requires_grad_(True) if t.is_floating_point() and "running" not in k
              and k != "head.dfl.conv.weight" else t.clone()) for k, t in sd.items()}
@@ -145,17 +162,18 @@ def cpu_baseline_train(version, nc, size, batch=4, steps=4):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": torch.get_num_threads(),
+    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads,
             "kind": "port", "sample": f"oracle/model_ref.py train step (fwd+bwd+SGD), fp32, B={batch}, "
-            f"{size}x{size}, {steps} timed steps after 1 warmup, host={os.cpu_count()} cpus"}
+            f"{size}x{size}, {steps} timed steps after 1 warmup ({dt:.1f} s), torch threads={threads} "
+            f"(OMP_NUM_THREADS share of a host reporting {os.cpu_count()} cpus)"}
 
 
-def cpu_baseline_infer(version, nc, size, batch=4, steps=3):
-    import numpy as np
+def cpu_baseline_infer(version, nc, size, batch=8, steps=12):
     from oracle import model_ref as M
     from oracle import nms as onms
     sd = M.init_params(version, nc)
     x = torch.randn(batch, 3, size, size, generator=torch.Generator().manual_seed(0))
+    threads = cpu_threads()
 
     def step():
         with torch.no_grad():
@@ -168,8 +186,9 @@ def cpu_baseline_infer(version, nc, size, batch=4, steps=3):
     for _ in range(steps):
         step()
     dt = time.perf_counter() - t0
-    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": torch.get_num_threads(),
-            "kind": "port", "sample": f"oracle eval forward + C NMS, fp32, B={batch}, {steps} timed steps"}
+    return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads,
+            "kind": "port", "sample": f"oracle eval forward + C NMS (1 core), fp32, B={batch}, {steps} timed steps "
+            f"({dt:.1f} s), torch threads={threads}"}
 
 
 def main():
@@ -177,7 +196,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if world > 1:
+    # under torchrun (even --nproc-per-node 1) the DP path runs: RCCL process group, bucketed
+    # all-reduce hook inside the plan backward, side-stream joins
+    distributed = world > 1 or "LOCAL_RANK" in os.environ
+    if distributed:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -195,7 +217,7 @@ def main():
     model.head.stride = torch.tensor([8.0, 16.0, 32.0])
     set_compute_dtype(model, dtype)
     net = model
-    if world > 1:
+    if distributed:
         from yms.dist import DataParallel
         net = DataParallel(model)
     result = {}
@@ -217,8 +239,8 @@ def main():
             opt.step()
 
         log(f"[rank {rank}] train warmup {a.warmup} + {a.steps} steps, B={a.batch}/GPU")
-        dt = timed(train_step, a.steps, a.warmup, world)
-        result["train"] = {"dt": dt, "img_s": world * a.batch * a.steps / dt,
+        dt, med = timed(train_step, a.steps, a.warmup, world)
+        result["train"] = {"dt": dt, "med_ms": med, "img_s": world * a.batch * a.steps / dt,
                            "peak_gb": torch.cuda.max_memory_allocated() / 2**30}
         log(f"[rank {rank}] train: {result['train']['img_s']:.1f} img/s ({dt / a.steps * 1e3:.1f} ms/step)")
         if rank == 0 and not a.no_profile:
@@ -244,8 +266,8 @@ def main():
             y = imodel(xi)
             yops.batched_nms_indices(y, 0.25, 0.45)
 
-        dti = timed(infer_step, a.steps, a.warmup, 1)
-        result["infer"] = {"dt": dti, "img_s": a.infer_batch * a.steps / dti}
+        dti, medi = timed(infer_step, a.steps, a.warmup, 1)
+        result["infer"] = {"dt": dti, "med_ms": medi, "img_s": a.infer_batch * a.steps / dti}
         log(f"[rank 0] infer: {result['infer']['img_s']:.1f} img/s ({dti / a.steps * 1e3:.2f} ms/batch)")
         if not a.no_profile:
             _lib.profile_begin()
@@ -263,6 +285,7 @@ def main():
             tr = result["train"]
             line["value"] = round(tr["img_s"], 2)
             line["ms_per_step"] = round(tr["dt"] / a.steps * 1e3, 3)
+            line["ms_per_step_median"] = round(tr["med_ms"], 3)
             tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L"}.get(
                 a.version, f"custom: YOLO-MS-{a.version.upper()}")
             line["config"] = {"workload": f"{tcfg} (reference YOLOv8-'{a.version}' graph) "
@@ -284,6 +307,7 @@ def main():
                 icfg += f" (YOLO-MS-{a.version.upper()} graph)"
             inf = {"value": round(result["infer"]["img_s"], 2), "unit": "images/sec",
                    "ms_per_batch": round(result["infer"]["dt"] / a.steps * 1e3, 3),
+                   "ms_per_batch_median": round(result["infer"]["med_ms"], 3),
                    "workload": f"{icfg}: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU "
                                "(forward + decode + class-wise NMS)"}
             if "infer_prof" in result:
@@ -311,7 +335,7 @@ def main():
                 for k, v in sorted(result[key].items(), key=lambda kv: -kv[1][1]):
                     log(f"  {k:28s} {v[0]:5d} {v[1]:9.3f} ms {v[2] / 1e9:9.1f}")
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.barrier()
         dist.destroy_process_group()
 

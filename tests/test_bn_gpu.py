@@ -1,0 +1,70 @@
+"""BN(+SiLU) backward through the C-ABI (reduce -> finalize -> apply) against an fp64 torch
+reference of nn.BatchNorm2d's training backward (components.py:73-74), at pixel counts where
+the 512-row partial-sum cap applies and does not divide npix (B=7 / B=9 at 640^2
+stride-8 layers), plus small and ragged counts.  The partial-sum scratch is pre-filled with NaN,
+so a finalize that read rows the reduce did not write fails loudly."""
+import ctypes
+
+import pytest
+import torch
+
+from yms import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(z, gy, sc, sh, mu, istd, act):
+    a = z * sc + sh
+    if act:
+        s = torch.sigmoid(a)
+        da = gy * (s * (1 + a * (1 - s)))
+    else:
+        da = gy
+    xh = (z - mu) * istd
+    dbeta = da.sum(0)
+    dgamma = (da * xh).sum(0)
+    n = z.shape[0]
+    dz = sc * (da - dbeta / n - xh * (dgamma / n))
+    return dgamma, dbeta, dz
+
+
+@pytest.mark.parametrize("npix,c,act", [(44800, 64, 1), (57600, 32, 1), (40001, 24, 0), (100, 16, 1),
+                                        (7 * 80 * 80, 128, 1)])
+def test_bn_bwd_matches_fp64(npix, c, act):
+    g = torch.Generator().manual_seed(npix + c)
+    z = torch.randn(npix, c, generator=g, dtype=torch.float64)
+    gy = torch.randn(npix, c, generator=g, dtype=torch.float64)
+    sc = torch.rand(c, generator=g, dtype=torch.float64) + 0.5
+    sh = torch.randn(c, generator=g, dtype=torch.float64) * 0.2
+    mu = z.mean(0)
+    istd = 1.0 / (z.var(0, unbiased=False) + 1e-3).sqrt()
+    dg, db, dz = _ref(z, gy, sc, sh, mu, istd, act)
+    dev = "cuda"
+    zd, gyd = z.float().to(dev), gy.float().to(dev)
+    scd, shd = sc.float().to(dev), sh.float().to(dev)
+    mi = torch.cat([mu, istd]).float().to(dev)
+    rows = L.lib().yms_bn_bwd_rows(npix)
+    assert rows >= 1
+    ws = torch.full((rows + 16, 2, c), float("nan"), dtype=torch.float32, device=dev)   # NaN beyond `rows`
+    dgd = torch.empty(c, device=dev)
+    dbd = torch.empty(c, device=dev)
+    coef = torch.empty(2 * c, device=dev)
+    out = torch.empty_like(zd)
+    st = L.stream_ptr()
+    L.call("yms_bn_act_bwd_reduce", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0, scd.data_ptr(),
+           shd.data_ptr(), mi.data_ptr(), act, ws.data_ptr(), st)
+    L.call("yms_bn_act_bwd_finalize", c, ws.data_ptr(), rows, npix, dgd.data_ptr(), dbd.data_ptr(),
+           coef.data_ptr(), st)
+    L.call("yms_bn_act_bwd_apply", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0, scd.data_ptr(),
+           shd.data_ptr(), mi.data_ptr(), coef.data_ptr(), act, out.data_ptr(), c, 0, None, 0, 0, 0, st)
+    torch.cuda.synchronize()
+    # rows the reduce wrote are exactly [0, rows): the NaN tail is untouched and nothing is NaN
+    assert torch.isnan(ws[rows:]).all()
+    assert torch.isfinite(ws[:rows]).all()
+
+    def rel(a, b):
+        return ((a.double().cpu() - b).norm() / b.norm()).item()
+
+    assert rel(dgd, dg) < 1e-5
+    assert rel(dbd, db) < 1e-5
+    assert rel(out, dz) < 1e-5

@@ -49,6 +49,18 @@ def test_host_shape_validation_and_sizes():
     assert L.lib().yms_nms_ws_bytes(32, 8400, 80) > 32 * 8400 * 28
 
 
+def test_bn_bwd_rows_is_the_launched_block_count():
+    """yms_bn_bwd_rows = the number of partial rows the reduce writes: with
+    ppb = ceil(npix / min(512, ceil(npix/64))) the launch covers ceil(npix / ppb) blocks."""
+    for npix in (1, 63, 64, 65, 100, 32768, 32769, 40001, 44800, 57600, 63 * 640, 7 * 80 * 80, 64 * 160 * 160):
+        rows = L.lib().yms_bn_bwd_rows(npix)
+        cap = min(512, (npix + 63) // 64)
+        ppb = -(-npix // cap)
+        assert rows == -(-npix // ppb), npix
+        assert 1 <= rows <= 512 and (rows - 1) * ppb < npix <= rows * ppb, npix
+    assert L.lib().yms_bn_bwd_rows(44800) == 510
+
+
 def test_null_pointers_rejected_without_gpu():
     sh = L.ConvShape(1, 8, 8, 8, 8, 3, 1, 1, 8, 8, L.F32)
     assert L.lib().yms_conv_fwd(ctypes.pointer(sh), None, 8, 0, None, None, 8, 0, None, None, 0, None, 0, 0,

@@ -108,3 +108,40 @@ def test_bucketed_allreduce_gloo_world2():
         assert ok_bcast, rank
         # rank 0's buffer (5.0) broadcast before forward, then BN2d(momentum 0.1) on zeros
         assert abs(rm - 0.9 * 5.0) < 1e-5, rm
+
+
+def test_bucket_layout_on_the_real_plan():
+    """Bucket readiness on the real YOLO-MS-S training plan (meta tensors, no GPU): the buckets tile
+    the flat fp32 grad arena in backward-completion order, and each is triggered only after the
+    last op owning any of its parameters (so no all-reduce starts before its grads are written)."""
+    from yms import runner
+    from yms.dist import GradBucketer
+    from yolov8.yolov8 import YOLOv8
+    m = YOLOv8("s", 80).train()
+    plan = runner.get_plan(m, [torch.empty(64, 3, 640, 640, device="meta")], torch.bfloat16, True)
+    params = plan.params()
+    views = [torch.empty(p.shape, device="meta") if p.requires_grad else None for p in params]
+    bk = GradBucketer(bucket_cap_mb=4.0)
+    buckets, ready, pos = bk._buckets(plan, views)
+    total = sum(v.numel() for v in views if v is not None)
+    assert abs(total - 10_497_808) < 100            # SURVEY 2.1: YOLOv8-s grads (DFL conv frozen)
+    assert buckets[0][0] == 0 and buckets[-1][1] == total
+    assert all(buckets[i][1] == buckets[i + 1][0] for i in range(len(buckets) - 1))
+    assert len(buckets) >= 8
+    owner = {}
+    for p_, op in enumerate(reversed(plan.ops)):
+        for pi in op.grad_params():
+            owner[pi] = max(owner.get(pi, -1), p_)
+    off = 0
+    ranges = []
+    for i in plan.pgrad_order:
+        if views[i] is not None:
+            ranges.append((i, off, off + views[i].numel()))
+            off += views[i].numel()
+    for a, b, trig in buckets:
+        for i, lo, hi in ranges:
+            if lo < b and a < hi:
+                assert owner[i] <= trig
+    # every bucket is launched exactly once over a backward walk
+    fired = [bi for p_ in range(len(plan.ops)) for bi in ready.get(p_, [])]
+    assert sorted(fired) == list(range(len(buckets)))

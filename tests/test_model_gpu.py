@@ -137,8 +137,17 @@ def test_full_model_fp32_vs_reference_golden(fname, v, nc):
             assert _maxerr(dict(m.named_buffers())[k[4:]], g[k]) < 1e-5, k
 
 
+def _quantiles_no_worse(ours, cpu, qs=(0.5, 0.9, 0.99), factor=1.3):
+    for q in qs:
+        a, b = torch.quantile(ours, q).item(), torch.quantile(cpu, q).item()
+        assert a <= factor * b + 1e-5, (q, a, b)
+
+
 def test_s640_bf16_eval_against_oracle():
-    """YOLO-MS-S (= YOLOv8-s graph) 640x640 bf16 inference vs the fp32 CPU oracle."""
+    """configs[1] graph: YOLO-MS-S (= YOLOv8-s graph) 640x640 bf16 inference vs the fp32 CPU oracle.
+    Gate: the error distribution (median / p90 / p99 of |ours - fp32 oracle| over class
+    probabilities, and the box L2 drift) within 1.3x of the reference's own CPU bf16 autocast path
+    on the same input (SURVEY 7.3 measured that path's class drift at 1.9e-3)."""
     v, nc = "s", 80
     sd = M.init_params(v, nc)
     m = YOLOv8(v, nc).to(DEV)
@@ -150,12 +159,14 @@ def test_s640_bf16_eval_against_oracle():
         y = m(x.to(DEV)).cpu()
     with torch.no_grad():
         ref = M.forward(dict(sd), v, nc, x, False)
+        with torch.autocast("cpu", dtype=torch.bfloat16):
+            cpu_bf = M.forward(dict(sd), v, nc, x, False).float()
     assert y.shape == (2, 8400, 84) and y.dtype == torch.float32
-    cls_err = (y[..., 4:] - ref[..., 4:]).abs().max().item()
-    box_rel = _rel(y[..., :4], ref[..., :4])
-    # bf16 end-to-end drift (CPU bf16 autocast itself drifts 4.5e-2 box / 1.9e-3 cls)
-    assert cls_err < 3e-2, cls_err
-    assert box_rel < 2e-2, box_rel
+    ours = (y[..., 4:] - ref[..., 4:]).abs().flatten()
+    cpu = (cpu_bf[..., 4:] - ref[..., 4:]).abs().flatten()
+    _quantiles_no_worse(ours, cpu)
+    assert ours.max().item() <= 1.5 * cpu.max().item() + 1e-4, (ours.max().item(), cpu.max().item())
+    assert _rel(y[..., :4], ref[..., :4]) <= 1.3 * _rel(cpu_bf[..., :4], ref[..., :4]) + 1e-4
 
 
 def _oracle_grads(v, nc, sd, x, dtype, autocast=False):
@@ -330,3 +341,219 @@ def test_l_bf16_train_grads_no_worse_than_cpu_bf16():
     assert ours[med] <= 1.2 * cpu[med], (ours[med], cpu[med])
     assert ours[p90] <= 1.2 * cpu[p90], (ours[p90], cpu[p90])
     assert ours[-1] <= 1.5 * cpu[-1], (ours[-1], cpu[-1])
+
+
+# ---- BASELINE.json configs at their own sizes (VERDICT r1 "untested configs") ---------------
+
+def _train_grads_vs(v, nc, sd, x, dtype):
+    m = YOLOv8(v, nc).to(DEV)
+    m.load_state_dict(sd)
+    m.train()
+    if dtype == torch.float32:
+        outs = m(x.to(DEV))
+    else:
+        with torch.autocast("cuda", dtype=dtype):
+            outs = m(x.to(DEV))
+    sum((o.double() ** 2).mean() for o in outs).backward()
+    return m, [o.detach().float().cpu() for o in outs], dict(m.named_parameters())
+
+
+def test_configs0_n320_fp32_eval_train_grads():
+    """configs[0]: YOLO-MS-XS -> reference 'n' graph, 320x320, B=2, fp32: eval output, train-mode
+    head maps, every parameter gradient and the BN running buffers against the oracle within the
+    north-star 1e-3 (grads against fp64, as the oracle's own fp32 noise is ~1e-4 there)."""
+    v, nc = "n", 80
+    sd = M.init_params(v, nc)
+    x = torch.randn(2, 3, 320, 320, generator=torch.Generator().manual_seed(10))
+    m = YOLOv8(v, nc).to(DEV)
+    m.load_state_dict(sd)
+    m.eval()
+    m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    y = m(x.to(DEV)).cpu()
+    with torch.no_grad():
+        ref = M.forward(dict(sd), v, nc, x, False)
+    assert y.shape == (2, 2100, 84)
+    assert (y[..., 4:] - ref[..., 4:]).abs().max().item() < 1e-3
+    assert _rel(y[..., :4], ref[..., :4]) < 1e-4
+    # train mode: head maps vs the fp32 oracle, grads vs fp64, running buffers
+    p = {k: (t.clone().requires_grad_(True) if t.is_floating_point() and "running" not in k
+             and k != "head.dfl.conv.weight" else t.clone()) for k, t in sd.items()}
+    r = M.forward(p, v, nc, x, True)
+    g64 = _oracle_grads(v, nc, sd, x, torch.float64)
+    m2, outs, pd = _train_grads_vs(v, nc, sd, x, torch.float32)
+    for o, rr in zip(outs, r):
+        assert _maxerr(o, rr.detach()) < 1e-3
+    worst = max(_rel(pd[k].grad, g64[k]) for k in g64 if k in pd)
+    assert worst < 1e-3, worst
+    bufs = dict(m2.named_buffers())
+    for k, t in p.items():
+        if "running" in k:
+            assert _maxerr(bufs[k], t) < 1e-4, k
+
+
+def _bf16_grads_vs_cpu_bf16(v, size, seed):
+    nc = 80
+    sd = M.init_params(v, nc)
+    x = torch.randn(2, 3, size, size, generator=torch.Generator().manual_seed(seed))
+    g64 = _oracle_grads(v, nc, sd, x, torch.float64)
+    gbf = _oracle_grads(v, nc, sd, x, torch.float32, autocast=True)
+    _, _, pd = _train_grads_vs(v, nc, sd, x, torch.bfloat16)
+    keys = [k for k in g64 if k in pd]
+    assert len(keys) == len([p for p in pd.values() if p.requires_grad])
+    ours = sorted(_rel(pd[k].grad, g64[k]) for k in keys)
+    cpu = sorted(_rel(gbf[k], g64[k]) for k in keys)
+    med, p90 = len(ours) // 2, (9 * len(ours)) // 10
+    assert ours[med] <= 1.2 * cpu[med], (ours[med], cpu[med])
+    assert ours[p90] <= 1.2 * cpu[p90], (ours[p90], cpu[p90])
+    assert ours[-1] <= 1.5 * cpu[-1], (ours[-1], cpu[-1])
+
+
+def test_configs2_s640_bf16_train_grads_no_worse_than_cpu_bf16():
+    """configs[2] at its own resolution: YOLO-MS-S 640x640 bf16 training gradients (B=2), drift
+    against fp64 no worse than the reference's CPU bf16 autocast path (median/p90 1.2x, worst 1.5x)."""
+    _bf16_grads_vs_cpu_bf16("s", 640, 21)
+
+
+def test_configs3_l640_fp32_train_grads_vs_fp64_and_bf16_drift():
+    """configs[3] at its own resolution: YOLO-MS-L 640x640 training (B=2).  fp32: every parameter
+    gradient within the north-star 1e-3 of an fp64 oracle.  bf16: with this init the L graph at
+    640^2 is chaotic under bf16 rounding -- the reference's own CPU bf16 autocast path drifts by a
+    median ~50% from fp64 on the parameter gradients -- so a full-model bf16 gradient gate measures
+    the dtype, not the kernels; the bf16 kernels are gated per layer at the exact B=64 L shapes in
+    test_configs_b64_bf16_layers_vs_fp32[l].  Here the bf16 gradients must only be finite with the
+    CPU bf16 path's order of drift (median within 3x)."""
+    v, nc = "l", 80
+    sd = M.init_params(v, nc)
+    x = torch.randn(2, 3, 640, 640, generator=torch.Generator().manual_seed(22))
+    g64 = _oracle_grads(v, nc, sd, x, torch.float64)
+    _, _, pd = _train_grads_vs(v, nc, sd, x, torch.float32)
+    keys = [k for k in g64 if k in pd]
+    assert len(keys) == len([p for p in pd.values() if p.requires_grad])
+    errs = sorted((_rel(pd[k].grad, g64[k]), k) for k in keys)
+    assert errs[-1][0] < 1e-3, errs[-3:]
+    gbf = _oracle_grads(v, nc, sd, x, torch.float32, autocast=True)
+    _, _, pdb = _train_grads_vs(v, nc, sd, x, torch.bfloat16)
+    assert all(torch.isfinite(pdb[k].grad).all() for k in keys)
+    ours = sorted(_rel(pdb[k].grad, g64[k]) for k in keys)
+    cpu = sorted(_rel(gbf[k], g64[k]) for k in keys)
+    med = len(ours) // 2
+    print(f"L640 bf16 grad drift vs fp64: ours median {ours[med]:.3g} p90 {ours[9 * len(ours) // 10]:.3g}; "
+          f"CPU bf16 median {cpu[med]:.3g} p90 {cpu[9 * len(cpu) // 10]:.3g}")
+    assert ours[med] <= 3.0 * cpu[med], (ours[med], cpu[med])
+
+
+def test_configs2_s640_b64_fp32_train_step_vs_oracle():
+    """The bench's batch: YOLO-MS-S 640x640, B=64, fp32 training forward + backward against the fp32
+    oracle at B=64.  Covers what only the full batch reaches: 256-row tiles with per-128-row BN
+    statistics, multi-split wgrad slabs, the capped (<= 512-row) BN-backward partial sums and
+    > 2^31-byte arenas.  Gate: head maps within 1e-3 (rel to max) and every parameter gradient
+    within 2e-3 relative L2 (two fp32 summation orders over 26 M pixels per channel)."""
+    v, nc = "s", 80
+    sd = M.init_params(v, nc)
+    x = torch.randn(64, 3, 640, 640, generator=torch.Generator().manual_seed(23))
+    p = {k: (t.clone().requires_grad_(True) if t.is_floating_point() and "running" not in k
+             and k != "head.dfl.conv.weight" else t.clone()) for k, t in sd.items()}
+    r = M.forward(p, v, nc, x, True)
+    sum((o.double() ** 2).mean() for o in r).backward()
+    rd = [o.detach() for o in r]
+    del r
+    _, outs, pd = _train_grads_vs(v, nc, sd, x, torch.float32)
+    for o, rr in zip(outs, rd):
+        assert _maxerr(o, rr) < 1e-3
+    errs = sorted((_rel(pd[k].grad, t.grad.double()), k) for k, t in p.items() if t.grad is not None)
+    assert errs[-1][0] < 2e-3, errs[-3:]
+
+
+def _gemm_conv(x, w, s):
+    """fp32 conv as unfold + GEMM on the GPU (torch im2col + BLAS; no conv library involved)."""
+    import torch.nn.functional as F
+    n, cin, h, wd = x.shape
+    cout, _, k, _ = w.shape
+    ho, wo = (h + 2 * (k // 2) - k) // s + 1, (wd + 2 * (k // 2) - k) // s + 1
+    cols = F.unfold(x, k, padding=k // 2, stride=s)                    # [n, cin*k*k, L]
+    return (w.view(cout, -1) @ cols).view(n, cout, ho, wo)
+
+
+def _gemm_conv_bwd(x, w, dz, s):
+    import torch.nn.functional as F
+    n, cin, h, wd = x.shape
+    cout, _, k, _ = w.shape
+    dzf = dz.reshape(n, cout, -1)                                        # [n, cout, L]
+    dcols = w.view(cout, -1).t() @ dzf                                   # [n, cin*k*k, L]
+    dx = F.fold(dcols, (h, wd), k, padding=k // 2, stride=s)
+    del dcols
+    cols = F.unfold(x, k, padding=k // 2, stride=s)
+    dw = torch.einsum("nol,nkl->ok", dzf, cols).view(cout, cin, k, k)
+    return dx, dw
+
+
+@pytest.mark.parametrize("version", ["s", "l"])
+def test_configs_b64_bf16_layers_vs_fp32(version):
+    """Every distinct conv layer of YOLO-MS-S (configs[2]) / YOLO-MS-L (configs[3]) at 640x640, B=64 in bf16 -- forward with BN
+    statistics, dgrad and wgrad -- through the C-ABI against fp32 PyTorch convolution on the GPU
+    over the same bf16-rounded operands (the per-kernel reference of a floating-point kernel).
+    These are the bench's exact shapes: 256-row tiles, split-K wgrad slab counts, 32-bit offsets."""
+    import ctypes
+
+    from hiputil import nhwc, pack, shape
+    from yms import _lib as L
+    from yms import runner
+    m = YOLOv8(version, 80)
+    m.train()
+    plan = runner.get_plan(m, [torch.empty(64, 3, 640, 640, device="meta")], torch.bfloat16, True)
+    seen = set()
+    g = torch.Generator(device=DEV).manual_seed(31)
+    dt = torch.bfloat16
+    for op in plan.ops:
+        sh = getattr(op, "shape", None)
+        if sh is None:
+            continue
+        key = (sh.n, sh.h, sh.w, sh.cin, sh.cout, sh.k, sh.stride)
+        if key in seen:
+            continue
+        seen.add(key)
+        n, h, w, cin, cout, k, s = key
+        x = torch.randn(n, cin, h, w, device=DEV, generator=g).to(dt)
+        wt = (torch.randn(cout, cin, k, k, device=DEV, generator=g) / (cin * k * k) ** 0.5).to(dt)
+        shp = shape(n, h, w, cin, cout, k, s, dt)
+        sp = ctypes.pointer(shp)
+        xb = nhwc(x.float(), dt)
+        # forward (+ BN partial statistics)
+        wp = pack(wt.float(), shp, dt, 0)
+        y = torch.zeros((n, shp.ho, shp.wo, (cout + 7) // 8 * 8), dtype=dt, device=DEV)
+        rows, ld = L.lib().yms_conv_stats_rows(sp), L.lib().yms_conv_stats_ld(sp)
+        st = torch.zeros((rows, 2, ld), dtype=torch.float32, device=DEV)
+        L.call("yms_conv_fwd", sp, xb.data_ptr(), xb.shape[-1], 0, wp.data_ptr(), y.data_ptr(), y.shape[-1], 0,
+               None, None, 0, None, 0, 0, st.data_ptr(), L.stream_ptr())
+        z = _gemm_conv(x.float(), wt.float(), s)
+        zs = z.abs().max().item()
+        err = (y[..., :cout].permute(0, 3, 1, 2).float() - z).abs().max().item()
+        assert err <= 1e-2 * zs, (key, "fwd", err, zs)
+        s1 = st[:, 0, :cout].double().sum(0)
+        s2 = st[:, 1, :cout].double().sum(0)
+        zd = z.double()
+        assert _rel(s1, zd.sum((0, 2, 3)).cpu()) < 1e-3, (key, "sum")
+        assert _rel(s2, (zd * zd).sum((0, 2, 3)).cpu()) < 1e-3, (key, "sumsq")
+        del z, zd
+        # dgrad / wgrad
+        dz = torch.randn(n, cout, shp.ho, shp.wo, device=DEV, generator=g).to(dt)
+        ref_dx, ref_dw = _gemm_conv_bwd(x.float(), wt.float(), dz.float(), s)
+        dzb = nhwc(dz.float(), dt)
+        if cin > 3:
+            wpt = pack(wt.float(), shp, dt, 1)
+            dx = torch.zeros((n, h, w, (cin + 7) // 8 * 8), dtype=dt, device=DEV)
+            L.call("yms_conv_dgrad", sp, dzb.data_ptr(), dzb.shape[-1], 0, wpt.data_ptr(), dx.data_ptr(),
+                   dx.shape[-1], 0, 0, L.stream_ptr())
+            err = (dx[..., :cin].permute(0, 3, 1, 2).float() - ref_dx).abs().max().item()
+            assert err <= 2e-2 * ref_dx.abs().max().item(), (key, "dgrad", err)
+            del dx
+        wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device=DEV)
+        dw = torch.zeros(cout, cin, k, k, device=DEV)
+        L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0,
+               ws.data_ptr(), wsb, dw.data_ptr(), 0, L.stream_ptr())
+        err = (dw - ref_dw).abs().max().item()
+        assert err <= 2e-3 * ref_dw.abs().max().item(), (key, "wgrad", err)
+        del x, wt, xb, y, st, dz, dzb, ws, dw, ref_dx, ref_dw
+        torch.cuda.empty_cache()
+    assert len(seen) >= 20

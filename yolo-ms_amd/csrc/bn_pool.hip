@@ -689,20 +689,23 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   return launch_status();
 }
 
-int yms_bn_bwd_rows(long npix) {
-  if (npix <= 0) return 0;
-  // partial-sum rows = reduce blocks, at most 512: 2 blocks per CU leave room for the
-  // side-stream wgrad and halve the finalize's table (interleaved A/B of the training step:
-  // cap 1024 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms; YMS_BN_BWD_ROWS_CAP overrides)
+// pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 512: 2 blocks
+// per CU leave room for the side-stream wgrad and halve the finalize's table (interleaved A/B of
+// the training step: cap 1024 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms;
+// YMS_BN_BWD_ROWS_CAP overrides)
+static long bwd_pix_per_block(long npix) {
   static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 512;
-  long rows = (npix + 63) / 64;
-  if (rows > cap) rows = cap;
-  return (int)rows;
+  const long rows = std::min(cap, (npix + 63) / 64);
+  return (npix + rows - 1) / rows;
 }
 
-static long bwd_pix_per_block(long npix) {
-  const int rows = yms_bn_bwd_rows(npix);
-  return (npix + rows - 1) / rows;
+// the number of partial rows the reduce WRITES = its launched block count ceil(npix / ppb).
+// Once the cap applies this can be below the cap (npix = 44800: ppb 88, 510 blocks), so the
+// scratch size, the launch and the finalize all use this one function.
+int yms_bn_bwd_rows(long npix) {
+  if (npix <= 0) return 0;
+  const long ppb = bwd_pix_per_block(npix);
+  return (int)((npix + ppb - 1) / ppb);
 }
 
 yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int z_ld, int z_off,

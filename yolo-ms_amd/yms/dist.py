@@ -47,11 +47,12 @@ class GradBucketer:
                 n = views[i].numel()
                 ranges.append((i, off, off + n))
                 off += n
-        # owner op position (in backward order) of every param
+        # owner op position (in backward order) of every param: the LAST op that writes its grad
+        # (a shared parameter is complete only after its final contribution)
         owner = {}
         for pos, op in enumerate(reversed(plan.ops)):
             for pi in op.grad_params():
-                owner.setdefault(pi, pos)
+                owner[pi] = max(owner.get(pi, -1), pos)
         buckets = []   # (start, end, ready_after_backward_pos)
         s, last = 0, -1
         for i, a, b in ranges:
