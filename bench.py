@@ -45,6 +45,11 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--mode", default="both", choices=["both", "train", "infer"])
+    ap.add_argument("--priority", type=int, default=1,
+                    help="run the step on a high-priority stream (the weight-gradient side stream keeps "
+                         "normal priority, so the critical path wins CU arbitration)")
+    ap.add_argument("--graph", type=int, default=0,
+                    help="replay each step as one captured HIP graph (1 GPU; the plans are static)")
     return ap.parse_args()
 
 
@@ -76,6 +81,24 @@ def timed(fn, steps, warmup, world):
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt, med = t[0].item(), t[1].item()
     return dt, med
+
+
+def graphed(step, warmup):
+    """Capture `step` (static inputs, static plan) as one HIP graph and return its replay.  The
+    warmup runs eagerly on a side stream first (optimizer state, packed-weight tables, plan caches
+    are created outside the capture)."""
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        for _ in range(max(warmup, 2)):
+            step()
+    torch.cuda.current_stream().wait_stream(s)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g):
+        step()
+    torch.cuda.synchronize()
+    return g.replay
 
 
 def add_traffic(roof, mode, workload):
@@ -206,6 +229,10 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    if a.priority:
+        # the critical path (forward, BN/dgrad backward chain) on a high-priority stream: it gets its
+        # own hardware queue and wins CU arbitration against the side-stream weight gradients
+        torch.cuda.set_stream(torch.cuda.Stream(device=dev, priority=-1))
     dtype = {"bf16": torch.bfloat16, "f16": torch.float16, "f32": torch.float32}[a.dtype]
 
     from yms import _lib, set_compute_dtype
@@ -238,9 +265,13 @@ def main():
             loss.backward()
             opt.step()
 
-        log(f"[rank {rank}] train warmup {a.warmup} + {a.steps} steps, B={a.batch}/GPU")
-        dt, med = timed(train_step, a.steps, a.warmup, world)
-        result["train"] = {"dt": dt, "med_ms": med, "img_s": world * a.batch * a.steps / dt,
+        run_train = train_step
+        use_graph = bool(a.graph) and not distributed
+        if use_graph:
+            run_train = graphed(train_step, a.warmup)
+        log(f"[rank {rank}] train warmup {a.warmup} + {a.steps} steps, B={a.batch}/GPU, graph={use_graph}")
+        dt, med = timed(run_train, a.steps, a.warmup, world)
+        result["train"] = {"dt": dt, "med_ms": med, "graph": use_graph, "img_s": world * a.batch * a.steps / dt,
                            "peak_gb": torch.cuda.max_memory_allocated() / 2**30}
         log(f"[rank {rank}] train: {result['train']['img_s']:.1f} img/s ({dt / a.steps * 1e3:.1f} ms/step)")
         if rank == 0 and not a.no_profile:
@@ -266,8 +297,10 @@ def main():
             y = imodel(xi)
             yops.batched_nms_indices(y, 0.25, 0.45)
 
-        dti, medi = timed(infer_step, a.steps, a.warmup, 1)
-        result["infer"] = {"dt": dti, "med_ms": medi, "img_s": a.infer_batch * a.steps / dti}
+        run_infer = graphed(infer_step, a.warmup) if a.graph else infer_step
+        dti, medi = timed(run_infer, a.steps, a.warmup, 1)
+        result["infer"] = {"dt": dti, "med_ms": medi, "graph": bool(a.graph),
+                           "img_s": a.infer_batch * a.steps / dti}
         log(f"[rank 0] infer: {result['infer']['img_s']:.1f} img/s ({dti / a.steps * 1e3:.2f} ms/batch)")
         if not a.no_profile:
             _lib.profile_begin()
@@ -296,7 +329,8 @@ def main():
                               "loss": "surrogate sum(mean(o^2)) over the 3 head maps (reference loss "
                                       "crashes for nc=80, SURVEY 0.5)",
                               "conv_gflop_per_img_fwd": round(flops_img / 1e9, 3),
-                              "peak_hbm_gib": round(tr["peak_gb"], 2)}
+                              "peak_hbm_gib": round(tr["peak_gb"], 2),
+                              "hip_graph": tr["graph"]}
             if "train_prof" in result:
                 line["roofline"] = conv_roofline(result["train_prof"], "conv implicit-GEMM fwd+dgrad+wgrad "
                                                  f"({a.dtype} MFMA), one training step")
@@ -309,7 +343,7 @@ def main():
                    "ms_per_batch": round(result["infer"]["dt"] / a.steps * 1e3, 3),
                    "ms_per_batch_median": round(result["infer"]["med_ms"], 3),
                    "workload": f"{icfg}: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU "
-                               "(forward + decode + class-wise NMS)"}
+                               "(forward + decode + class-wise NMS)", "hip_graph": result["infer"]["graph"]}
             if "infer_prof" in result:
                 inf["roofline"] = conv_roofline(result["infer_prof"], f"conv implicit-GEMM fwd ({a.dtype} MFMA)")
                 add_traffic(inf["roofline"], "infer", inf["workload"])

@@ -67,7 +67,9 @@ yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* p
 
 /* Batched packing (one launch for all of a plan's packs; training repacks every step).
  * yms_pack_job_init fills a job on the host (YMS_ERR_UNSUPPORTED for stride-2 dgrad packs,
- * which keep yms_conv_pack_weight); the job array must be in device memory for the launch. */
+ * which keep yms_conv_pack_weight); the job array must be in device memory for the launch.
+ * Each job's `packed` is taken as a byte offset from dst_base (dst_base NULL: absolute), so one
+ * device job table serves every arena (and HIP-graph capture needs no host->device copy). */
 typedef struct {
   const float* w;
   void* packed;
@@ -75,7 +77,7 @@ typedef struct {
 } yms_pack_job;
 yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* packed, int for_dgrad,
                              yms_pack_job* job);
-yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* stream);
+yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* dst_base, void* stream);
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------------------- */
 /* Number of fp32 rows of BN partial statistics written by yms_conv_fwd(stats != NULL);
@@ -120,7 +122,7 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
  *   finalize: dgamma, dbeta (+=) and the two per-channel coefficients
  *   apply: dz = scale*(da - mean(da) - xhat*mean(da*xhat)), written over dz (may alias z);
  *          gres = gy (gres_acc=0) or gres += gy (gres_acc=1) when gres != NULL (residual). */
-int yms_bn_bwd_rows(long npix);
+int yms_bn_bwd_rows(long npix, int c);   /* partial rows = reduce blocks; ws holds rows*2*c floats */
 yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
                                  const void* gy, int gy_ld, int gy_off, const float* scale,
                                  const float* shift, const float* mean_invstd, int act,
@@ -132,9 +134,18 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
                                 const float* shift, const float* mean_invstd, const float* coef,
                                 int act, void* dz, int dz_ld, int dz_off,
                                 void* gres, int gres_ld, int gres_off, int gres_acc, void* stream);
-/* Bias-only backward of the head's 1x1 nn.Conv2d: dbias (+)= sum over pixels of gy. */
+/* reduce + finalize in ONE launch: the last reduce block to finish (agent-scope release/acquire
+ * ticket on *counter) sums the partial rows.  *counter must be 0 on entry (it is 0 again on exit);
+ * dgamma/dbeta/coef as yms_bn_act_bwd_finalize (any may be NULL). */
+yms_status yms_bn_act_bwd_reduce_finalize(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                                          const void* gy, int gy_ld, int gy_off, const float* scale,
+                                          const float* shift, const float* mean_invstd, int act, float* ws,
+                                          unsigned* counter, float* dgamma, float* dbeta, float* coef,
+                                          void* stream);
+/* Bias-only backward of the head's 1x1 nn.Conv2d: dbias = sum over pixels of gy (one launch;
+ * counter as above). */
 yms_status yms_bias_bwd(int dtype, long npix, int c, const void* gy, int gy_ld, int gy_off,
-                        float* ws, float* dbias, void* stream);
+                        float* ws, unsigned* counter, float* dbias, void* stream);
 
 /* ---- SPPF pools / upsample / layout ---------------------------------------------------- */
 /* buf holds 4 consecutive channel slots of width c at channel offset off: slot0 = input x,

@@ -43,28 +43,55 @@ def test_bn_bwd_matches_fp64(npix, c, act):
     zd, gyd = z.float().to(dev), gy.float().to(dev)
     scd, shd = sc.float().to(dev), sh.float().to(dev)
     mi = torch.cat([mu, istd]).float().to(dev)
-    rows = L.lib().yms_bn_bwd_rows(npix)
+    rows = L.lib().yms_bn_bwd_rows(npix, c)
     assert rows >= 1
-    ws = torch.full((rows + 16, 2, c), float("nan"), dtype=torch.float32, device=dev)   # NaN beyond `rows`
-    dgd = torch.empty(c, device=dev)
-    dbd = torch.empty(c, device=dev)
-    coef = torch.empty(2 * c, device=dev)
-    out = torch.empty_like(zd)
     st = L.stream_ptr()
-    L.call("yms_bn_act_bwd_reduce", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0, scd.data_ptr(),
-           shd.data_ptr(), mi.data_ptr(), act, ws.data_ptr(), st)
-    L.call("yms_bn_act_bwd_finalize", c, ws.data_ptr(), rows, npix, dgd.data_ptr(), dbd.data_ptr(),
-           coef.data_ptr(), st)
-    L.call("yms_bn_act_bwd_apply", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0, scd.data_ptr(),
-           shd.data_ptr(), mi.data_ptr(), coef.data_ptr(), act, out.data_ptr(), c, 0, None, 0, 0, 0, st)
-    torch.cuda.synchronize()
-    # rows the reduce wrote are exactly [0, rows): the NaN tail is untouched and nothing is NaN
-    assert torch.isnan(ws[rows:]).all()
-    assert torch.isfinite(ws[:rows]).all()
 
     def rel(a, b):
         return ((a.double().cpu() - b).norm() / b.norm()).item()
 
-    assert rel(dgd, dg) < 1e-5
-    assert rel(dbd, db) < 1e-5
-    assert rel(out, dz) < 1e-5
+    for fused in (False, True):
+        ws = torch.full((rows + 16, 2, c), float("nan"), dtype=torch.float32, device=dev)   # NaN beyond `rows`
+        cnt = torch.zeros(4, dtype=torch.int32, device=dev)
+        dgd = torch.empty(c, device=dev)
+        dbd = torch.empty(c, device=dev)
+        coef = torch.empty(2 * c, device=dev)
+        out = torch.empty_like(zd)
+        if fused:
+            L.call("yms_bn_act_bwd_reduce_finalize", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0,
+                   scd.data_ptr(), shd.data_ptr(), mi.data_ptr(), act, ws.data_ptr(), cnt.data_ptr(), dgd.data_ptr(),
+                   dbd.data_ptr(), coef.data_ptr(), st)
+        else:
+            L.call("yms_bn_act_bwd_reduce", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0,
+                   scd.data_ptr(), shd.data_ptr(), mi.data_ptr(), act, ws.data_ptr(), st)
+            L.call("yms_bn_act_bwd_finalize", c, ws.data_ptr(), rows, npix, dgd.data_ptr(), dbd.data_ptr(),
+                   coef.data_ptr(), st)
+        L.call("yms_bn_act_bwd_apply", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0, scd.data_ptr(),
+               shd.data_ptr(), mi.data_ptr(), coef.data_ptr(), act, out.data_ptr(), c, 0, None, 0, 0, 0, st)
+        torch.cuda.synchronize()
+        # rows the reduce wrote are exactly [0, rows): the NaN tail is untouched and nothing is NaN
+        assert torch.isnan(ws[rows:]).all()
+        assert torch.isfinite(ws[:rows]).all()
+        assert int(cnt[0]) == 0          # the fused finalize leaves its counter at zero
+        assert rel(dgd, dg) < 1e-5, fused
+        assert rel(dbd, db) < 1e-5, fused
+        assert rel(out, dz) < 1e-5, fused
+
+
+def test_bias_bwd_fused():
+    g = torch.Generator().manual_seed(5)
+    npix, c = 64 * 20 * 20, 80
+    gy = torch.randn(npix, 88, generator=g, dtype=torch.float64)
+    dev = "cuda"
+    gyb = gy.to(torch.bfloat16).to(dev)
+    ref = gyb.double().cpu()[:, :c].sum(0)
+    rows = L.lib().yms_bn_bwd_rows(npix, c)
+    ws = torch.empty((rows, 2, c), dtype=torch.float32, device=dev)
+    cnt = torch.zeros(4, dtype=torch.int32, device=dev)
+    db = torch.empty(c, device=dev)
+    for _ in range(2):      # the counter is reusable: it returns to zero
+        L.call("yms_bias_bwd", L.BF16, npix, c, gyb.data_ptr(), 88, 0, ws.data_ptr(), cnt.data_ptr(), db.data_ptr(),
+               L.stream_ptr())
+        torch.cuda.synchronize()
+        assert ((db.double().cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-5
+        assert int(cnt[0]) == 0

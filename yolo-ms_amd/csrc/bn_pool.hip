@@ -191,11 +191,18 @@ __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const
 // BN + SiLU backward.  Each block owns a contiguous pixel range and writes one partial row
 // [2][c] (sum da, sum da*xhat) -- deterministic, no atomics.
 // ------------------------------------------------------------------------------------------
-template <typename T, bool HAS_Z>
+struct BwdFin {          // fused finalize (FIN): the last reduce block to finish sums every partial row
+  unsigned* cnt;        // arrival counter, zero on entry (the plan zeroes one per layer per backward)
+  float *dgamma, *dbeta, *coef;
+  long count;
+};
+
+template <typename T, bool HAS_Z, bool FIN = false>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld,
                                                             int z_off, const T* gy, int gy_ld, int gy_off,
                                                             const float* scale, const float* shift,
-                                                            const float* mi, int act, float* ws, long ppb) {
+                                                            const float* mi, int act, float* ws, long ppb,
+                                                            BwdFin fin = BwdFin{}) {
   __shared__ float red[2][2048 + 64];
   ChanMap m(c);
   const int c0 = m.g * 8, nv = min(8, c - c0);
@@ -267,6 +274,63 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
       }
     }
     __syncthreads();
+  }
+  if constexpr (FIN) {
+    // in-launch finalize (cdna_hip_programming.md G16 counter hand-off): every wave drains its
+    // partial-row stores, one agent-scope release + ticket; the block drawing the last ticket
+    // acquires and sums all rows in a fixed order (deterministic whichever block is last)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    unsigned* flag = reinterpret_cast<unsigned*>(&red[0][0]);
+    if (threadIdx.x == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const unsigned t = __hip_atomic_fetch_add(fin.cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned last = (t == gridDim.x - 1) ? 1u : 0u;
+      if (last) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (flag[0] == 0) return;
+    __syncthreads();
+    const int rows = gridDim.x, tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
+    double* dred = reinterpret_cast<double*>(&red[0][0]);     // [2][8][33] doubles
+    for (int cb = 0; cb < c; cb += 32) {
+      const int ch = cb + tx;
+      double b1[4] = {0, 0, 0, 0}, b2[4] = {0, 0, 0, 0};
+      if (ch < c) {
+        int r = ty;
+        for (; r + 24 < rows; r += 32) {
+#pragma unroll
+          for (int u = 0; u < 4; ++u) {
+            b1[u] += ws[(long)(r + 8 * u) * 2 * c + ch];
+            b2[u] += ws[(long)(r + 8 * u) * 2 * c + c + ch];
+          }
+        }
+        for (; r < rows; r += 8) {
+          b1[0] += ws[(long)r * 2 * c + ch];
+          b2[0] += ws[(long)r * 2 * c + c + ch];
+        }
+      }
+      dred[(0 * 8 + ty) * 33 + tx] = (b1[0] + b1[1]) + (b1[2] + b1[3]);
+      dred[(1 * 8 + ty) * 33 + tx] = (b2[0] + b2[1]) + (b2[2] + b2[3]);
+      __syncthreads();
+      if (ty == 0 && ch < c) {
+        double t1 = 0.0, t2 = 0.0;
+        for (int k = 0; k < 8; ++k) { t1 += dred[(0 * 8 + k) * 33 + tx]; t2 += dred[(1 * 8 + k) * 33 + tx]; }
+        if (fin.dbeta) fin.dbeta[ch] = (float)t1;
+        if (fin.dgamma) fin.dgamma[ch] = (float)t2;
+        if (fin.coef) {
+          fin.coef[ch] = (float)(t1 / (double)fin.count);
+          fin.coef[c + ch] = (float)(t2 / (double)fin.count);
+        }
+      }
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) __hip_atomic_store(fin.cnt, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
 
@@ -689,22 +753,24 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   return launch_status();
 }
 
-// pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 512: 2 blocks
-// per CU leave room for the side-stream wgrad and halve the finalize's table (interleaved A/B of
-// the training step: cap 1024 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms;
-// YMS_BN_BWD_ROWS_CAP overrides)
-static long bwd_pix_per_block(long npix) {
+// pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 512 (2 blocks
+// per CU leave room for the side-stream wgrad; interleaved A/B of the training step: cap 1024
+// 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms; YMS_BN_BWD_ROWS_CAP overrides) and at most
+// 32768 / c, so that the partial table the fused finalize's single block sums stays <= 256 KB.
+static long bwd_pix_per_block(long npix, int c) {
   static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 512;
-  const long rows = std::min(cap, (npix + 63) / 64);
+  static const long cprod = getenv("YMS_BN_BWD_CCAP") ? atol(getenv("YMS_BN_BWD_CCAP")) : 32768;   // dev A/B
+  const long ccap = cprod > 0 ? std::max(32l, cprod / std::max(c, 1)) : cap;
+  const long rows = std::max(1l, std::min(std::min(cap, ccap), (npix + 63) / 64));
   return (npix + rows - 1) / rows;
 }
 
 // the number of partial rows the reduce WRITES = its launched block count ceil(npix / ppb).
-// Once the cap applies this can be below the cap (npix = 44800: ppb 88, 510 blocks), so the
+// Once a cap applies this can be below the cap (npix = 44800, c = 64: ppb 88, 510 blocks), so the
 // scratch size, the launch and the finalize all use this one function.
-int yms_bn_bwd_rows(long npix) {
-  if (npix <= 0) return 0;
-  const long ppb = bwd_pix_per_block(npix);
+int yms_bn_bwd_rows(long npix, int c) {
+  if (npix <= 0 || c <= 0) return 0;
+  const long ppb = bwd_pix_per_block(npix, c);
   return (int)((npix + ppb - 1) / ppb);
 }
 
@@ -715,7 +781,7 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
   if (npix <= 0 || !gy || !ws || !vok(gy_ld, gy_off, c)) return YMS_ERR_INVALID;
   if (z && (!vok(z_ld, z_off, c) || !scale || !shift || !mean_invstd)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = bwd_pix_per_block(npix);
+  const long ppb = bwd_pix_per_block(npix, c);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
   if (z) {
     YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(rows), dim3(256), 0,
@@ -763,12 +829,35 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
   return launch_status();
 }
 
+yms_status yms_bn_act_bwd_reduce_finalize(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
+                                          const void* gy, int gy_ld, int gy_off, const float* scale,
+                                          const float* shift, const float* mean_invstd, int act, float* ws,
+                                          unsigned* counter, float* dgamma, float* dbeta, float* coef,
+                                          void* stream) {
+  if (npix <= 0 || !gy || !ws || !counter || !vok(gy_ld, gy_off, c)) return YMS_ERR_INVALID;
+  if (z && (!vok(z_ld, z_off, c) || !scale || !shift || !mean_invstd)) return YMS_ERR_INVALID;
+  if (c > 2048) return YMS_ERR_UNSUPPORTED;
+  const long ppb = bwd_pix_per_block(npix, c);
+  const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
+  const BwdFin fin{counter, dgamma, dbeta, coef, npix};
+  if (z) {
+    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true, true>), dim3(rows), dim3(256), 0,
+                                                 (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
+                                                 (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd,
+                                                 act, ws, ppb, fin));
+  } else {
+    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false, true>), dim3(rows), dim3(256), 0,
+                                                 (hipStream_t)stream, npix, c, (const T*)nullptr, 0, 0,
+                                                 (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd,
+                                                 act, ws, ppb, fin));
+  }
+  return launch_status();
+}
+
 yms_status yms_bias_bwd(int dtype, long npix, int c, const void* gy, int gy_ld, int gy_off,
-                        float* ws, float* dbias, void* stream) {
-  yms_status s = yms_bn_act_bwd_reduce(dtype, npix, c, nullptr, 0, 0, gy, gy_ld, gy_off, nullptr,
-                                       nullptr, nullptr, YMS_ACT_NONE, ws, stream);
-  if (s != YMS_OK) return s;
-  return yms_bn_act_bwd_finalize(c, ws, yms_bn_bwd_rows(npix), npix, nullptr, dbias, nullptr, stream);
+                        float* ws, unsigned* counter, float* dbias, void* stream) {
+  return yms_bn_act_bwd_reduce_finalize(dtype, npix, c, nullptr, 0, 0, gy, gy_ld, gy_off, nullptr, nullptr,
+                                        nullptr, YMS_ACT_NONE, ws, counter, nullptr, dbias, nullptr, stream);
 }
 
 size_t yms_sppf_ws_bytes(int n, int h, int w, int c) {

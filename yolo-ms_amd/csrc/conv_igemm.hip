@@ -1151,8 +1151,9 @@ __global__ void pack_weight_kernel(const float* w, T* out, int cout, int cin, in
 
 // All of a plan's weight packs in one launch (training repacks every step): block (x, job)
 // handles rows x, x + gridDim.x, ... of job `job`; 32-bit index math only.
-__global__ __launch_bounds__(256) void pack_weight_batched_kernel(const yms_pack_job* jobs) {
-  const yms_pack_job j = jobs[blockIdx.y];
+__global__ __launch_bounds__(256) void pack_weight_batched_kernel(const yms_pack_job* jobs, char* dst_base) {
+  yms_pack_job j = jobs[blockIdx.y];
+  j.packed = dst_base + (uintptr_t)j.packed;     // offsets relative to the (per-call) arena base
   const int kk = j.ks * j.ks;
   for (int r = blockIdx.x; r < j.rows; r += gridDim.x) {
     for (int k = threadIdx.x; k < j.kp_elems; k += 256) {
@@ -1467,7 +1468,7 @@ size_t yms_conv_packed_elems(const yms_conv_shape* s, int for_dgrad) {
 
 yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* packed, int for_dgrad,
                              yms_pack_job* job) {
-  if (!shape_ok(s) || !w || !packed || !job) return YMS_ERR_INVALID;
+  if (!shape_ok(s) || !w || !job) return YMS_ERR_INVALID;   // packed may be an offset (0 allowed)
   if (for_dgrad && s->stride == 2) return YMS_ERR_UNSUPPORTED;   // parity-class packing: yms_conv_pack_weight
   PackGeo g = pack_geo(s, for_dgrad);
   job->w = w;
@@ -1483,12 +1484,12 @@ yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* pack
   return YMS_OK;
 }
 
-yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* stream) {
+yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* dst_base, void* stream) {
   if (njobs < 0 || (njobs > 0 && !jobs_dev)) return YMS_ERR_INVALID;
   if (njobs == 0) return YMS_OK;
   if (njobs > 65535) return YMS_ERR_UNSUPPORTED;
   hipLaunchKernelGGL(pack_weight_batched_kernel, dim3(64, (unsigned)njobs), dim3(256), 0, (hipStream_t)stream,
-                     jobs_dev);
+                     jobs_dev, (char*)dst_base);
   return launch_status();
 }
 

@@ -52,7 +52,7 @@ _SIGS = {
     "yms_conv_packed_elems": (_SZ, [_SP, _I]),
     "yms_conv_pack_weight": (_I, [_SP, _P, _P, _I, _P]),
     "yms_pack_job_init": (_I, [_SP, _P, _P, _I, ctypes.POINTER(PackJob)]),
-    "yms_conv_pack_weights_batched": (_I, [_I, _P, _P]),
+    "yms_conv_pack_weights_batched": (_I, [_I, _P, _P, _P]),
     "yms_conv_stats_rows": (_I, [_SP]),
     "yms_conv_stats_ld": (_I, [_SP]),
     "yms_conv_fwd": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _P]),
@@ -62,12 +62,14 @@ _SIGS = {
     "yms_bn_fold": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
     "yms_bn_finalize": (_I, [_I, _P, _I, _I, _L, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P]),
     "yms_affine_act": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _I, _I, _P]),
-    "yms_bn_bwd_rows": (_I, [_L]),
+    "yms_bn_bwd_rows": (_I, [_L, _I]),
     "yms_bn_act_bwd_reduce": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
     "yms_bn_act_bwd_finalize": (_I, [_I, _P, _I, _L, _P, _P, _P, _P]),
     "yms_bn_act_bwd_apply": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _I, _P, _I, _I,
                                   _P, _I, _I, _I, _P]),
-    "yms_bias_bwd": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _P]),
+    "yms_bn_act_bwd_reduce_finalize": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P, _P, _P,
+                                            _P, _P]),
+    "yms_bias_bwd": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _P, _P]),
     "yms_sppf_ws_bytes": (_SZ, [_I, _I, _I, _I]),
     "yms_sppf_pool_fwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P]),
     "yms_sppf_pool_bwd": (_I, [_I, _I, _I, _I, _I, _P, _I, _I, _P, _I, _I, _P, _P]),

@@ -14,8 +14,9 @@ new DP layer of SURVEY 5/8(e):
   backward; ``finish`` joins the compute stream to every outstanding collective.
 * gradients reach autograd as views of the reduced arena -- no copies.
 
-xGMI is point-to-point (7 links per GPU); ~25 MB buckets give a few large ring
-collectives per step for YOLOv8-s (10.5 M params = 42 MB fp32).
+xGMI is point-to-point (7 links per GPU); ~10 MB buckets give 4-5 ring collectives per step
+for YOLOv8-s (10.5 M params = 42 MB fp32), the first one starting after about a fifth of the
+backward, each issued from the wgrad side stream so the compute stream never waits for it.
 """
 from __future__ import annotations
 
@@ -27,7 +28,7 @@ from torch import nn
 class GradBucketer:
     """Issues bucketed all-reduces from inside the plan backward (see runner._PlanFn)."""
 
-    def __init__(self, group=None, bucket_cap_mb=25.0):
+    def __init__(self, group=None, bucket_cap_mb=10.0):
         self.group = group
         self.cap = int(bucket_cap_mb * 1024 * 1024 / 4)
         self._plans = {}
@@ -105,7 +106,7 @@ class DataParallel(nn.Module):
     inside the reference training loop; state_dict keys are prefixed ``module.`` exactly
     like torch DDP (the reference strips that prefix when loading, train.py:270-276)."""
 
-    def __init__(self, module, group=None, bucket_cap_mb=25.0, broadcast_buffers=True):
+    def __init__(self, module, group=None, bucket_cap_mb=10.0, broadcast_buffers=True):
         super().__init__()
         if not dist.is_initialized():
             raise RuntimeError("yms.dist.DataParallel: call torch.distributed.init_process_group first")
@@ -116,11 +117,36 @@ class DataParallel(nn.Module):
         with torch.no_grad():
             for p in module.parameters():
                 dist.broadcast(p.data, 0, group=group)
+            self._flat_buffers()
             self._sync_buffers()
         module._yms_grad_hook = self.bucketer
 
+    def _flat_buffers(self):
+        """Re-home every floating-point buffer (BN running stats) as a view of ONE flat tensor, so
+        the per-step broadcast is a single in-place collective with no flatten/unflatten copies."""
+        mods = [(m, n, b) for m in self.module.modules() for n, b in m._buffers.items()
+                if b is not None and b.is_floating_point()]
+        self._flat = None
+        if not mods:
+            return
+        groups = {}
+        for m, n, b in mods:
+            groups.setdefault((b.dtype, b.device), []).append((m, n, b))
+        if len(groups) != 1:
+            self._bufs = [b for _, _, b in mods]
+            return
+        flat = torch._utils._flatten_dense_tensors([b for _, _, b in mods])
+        off = 0
+        for m, n, b in mods:
+            m._buffers[n] = flat[off:off + b.numel()].view_as(b)
+            off += b.numel()
+        self._flat = flat
+
     def _sync_buffers(self):
-        bufs = [b for n, b in self.module.named_buffers() if b.is_floating_point()]
+        if self._flat is not None:
+            dist.broadcast(self._flat, 0, group=self.group)
+            return
+        bufs = getattr(self, "_bufs", [])
         if not bufs:
             return
         flat = torch._utils._flatten_dense_tensors(bufs)

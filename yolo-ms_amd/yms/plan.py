@@ -22,12 +22,17 @@ contiguously -- see yms.dist).
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
 from . import _lib as L
 
 ALIGN = 256
+# BN backward finalize inside the reduce launch (last-arriving block, YMS_BN_FUSED=1) vs a separate
+# launch: the in-launch finalize puts one block's serial sum of the partial table on the critical path
+# (interleaved A/B, profiles/r02_ab_bn_fused_priority_graph.txt: 19.5-19.7 ms separate vs 20.4-21.3 ms fused)
+BN_FUSED_FINALIZE = os.environ.get("YMS_BN_FUSED", "0") == "1"
 BN_MOMENTUM = 0.03   # components.py:73
 BN_EPS = 1e-3
 
@@ -156,6 +161,10 @@ class Rt:
     def g(self, v):
         return self.gbase + v.buf.off
 
+    def cnt(self, i):
+        """Arrival counter i of the in-launch BN-backward finalize (zeroed at backward start)."""
+        return self.gbase + self.plan.gscratch["cnt"] + 16 * i
+
     def wst(self):
         """Stream for a weight-gradient GEMM (+ its split reduce): a side stream ordered after
         everything enqueued on the main stream so far.  wgrad is off the backward's critical
@@ -210,13 +219,15 @@ class ConvOp:
             self.stats_rows = L.lib().yms_conv_stats_rows(self.sp)
             self.stats_ld = L.lib().yms_conv_stats_ld(self.sp)
             plan.need_scratch("stats", 4 * 2 * self.stats_rows * self.stats_ld)
-            plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix))
+            plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
             plan.need_scratch("coef", 8 * c)
+            self.cnt = plan.counter()
             plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
 
-    def pack_specs(self, base):
+    def pack_specs(self):
+        """(shape, fp32 weight, arena byte offset of the packed copy, for_dgrad) per training pack."""
         w = self.mod.conv.weight.data_ptr()
-        return [(self.sp, w, base + self.t_wp, 0), (self.sp, w, base + self.t_wpt, 1)]
+        return [(self.sp, w, self.t_wp, 0), (self.sp, w, self.t_wpt, 1)]
 
     def prepare_eval(self, rt):
         m = self.mod
@@ -264,10 +275,16 @@ class ConvOp:
         ws = rt.gbase + rt.plan.gscratch["bwd"]
         coef = rt.gbase + rt.plan.gscratch["coef"]
         z = base + self.z
-        L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
-               base + self.sh, base + self.mi, self.act, ws, rt.st)
-        L.call("yms_bn_act_bwd_finalize", c, ws, L.lib().yms_bn_bwd_rows(self.npix), self.npix,
-               rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        if BN_FUSED_FINALIZE:
+            # one launch: partial sums + (last block) dgamma / dbeta / the two apply coefficients
+            L.call("yms_bn_act_bwd_reduce_finalize", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+                   base + self.sh, base + self.mi, self.act, ws, rt.cnt(self.cnt), rt.pgrad(self.pg),
+                   rt.pgrad(self.pb), coef, rt.st)
+        else:
+            L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+                   base + self.sh, base + self.mi, self.act, ws, rt.st)
+            L.call("yms_bn_act_bwd_finalize", c, ws, L.lib().yms_bn_bwd_rows(self.npix, c), self.npix,
+                   rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
         gres = rt.g(r) if r is not None else None
         gro = (r.buf.ld, r.off) if r is not None else (0, 0)
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
@@ -310,15 +327,16 @@ class BiasConvOp:
         if plan.training:
             self.t_wp = La.alloc(self.wp_elems * es)
             self.t_wpt = La.alloc(self.wpt_elems * es)
-            plan.need_scratch("bwd", 4 * 2 * self.c * L.lib().yms_bn_bwd_rows(self.npix))
+            plan.need_scratch("bwd", 4 * 2 * self.c * L.lib().yms_bn_bwd_rows(self.npix, self.c))
             plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
+            self.cnt = plan.counter()
 
     def prepare_eval(self, rt):
         L.call("yms_conv_pack_weight", self.sp, self.conv.weight.data_ptr(), rt.eval_base + self.e_wp, 0, rt.st)
 
-    def pack_specs(self, base):
+    def pack_specs(self):
         w = self.conv.weight.data_ptr()
-        return [(self.sp, w, base + self.t_wp, 0), (self.sp, w, base + self.t_wpt, 1)]
+        return [(self.sp, w, self.t_wp, 0), (self.sp, w, self.t_wpt, 1)]
 
     def fwd(self, rt):
         x, y = self.x, self.y
@@ -342,7 +360,7 @@ class BiasConvOp:
         db = rt.pgrad(self.pbias)
         if db is not None:
             L.call("yms_bias_bwd", rt.plan.dt, self.npix, self.c, gy, gyl, gyo,
-                   rt.gbase + rt.plan.gscratch["bwd"], db, rt.st)
+                   rt.gbase + rt.plan.gscratch["bwd"], rt.cnt(self.cnt), db, rt.st)
         if x.buf.needs_grad:
             L.call("yms_conv_dgrad", self.sp, gy, gyl, gyo, rt.base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
                    self.acc_x, rt.st)
@@ -472,6 +490,7 @@ class Plan:
         self.bufs, self.ops, self.param_refs = b.bufs, b.ops, b.param_refs
         self.inputs, self.outputs, self.kind = inputs, outputs, kind
         self.scratch_req = {}
+        self.n_counters = 0
         La, Le = Layout(), Layout()
         for buf in self.bufs:
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
@@ -486,6 +505,7 @@ class Plan:
         Lg = Layout()
         Lg.size = self.act_bytes
         self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf")}
+        self.gscratch["cnt"] = Lg.alloc(16 * max(self.n_counters, 1))
         self.garena_bytes = Lg.size
         self.eval_bytes = Le.size
         self.zero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.zero]
@@ -495,6 +515,7 @@ class Plan:
             for op in reversed(self.ops):
                 op.plan_grads(T)
             self.gzero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.idx in T.zero]
+            self.gzero_ranges.append((self.gscratch["cnt"], 16 * max(self.n_counters, 1)))
         self.flops = sum(op.flops for op in self.ops)
         # parameter-gradient arena in backward-completion order (reverse op order)
         order = []
@@ -507,6 +528,11 @@ class Plan:
         self.pgrad_order = order
         self._eval_sig = None
         self._eval_arena = None
+
+    def counter(self):
+        """Reserve one 16-B arrival counter in the grad scratch (-> its index)."""
+        self.n_counters += 1
+        return self.n_counters - 1
 
     def need_scratch(self, key, nbytes):
         self.scratch_req[key] = max(self.scratch_req.get(key, 0), int(nbytes))
@@ -540,9 +566,10 @@ class Plan:
 
     def prepack(self, rt):
         """Training: issue every conv weight pack of the step -- one batched launch for the
-        plain packs (device job table cached per arena base) plus the stride-2 dgrad parity
+        plain packs (device job table of arena OFFSETS, cached per parameter set, so it is valid
+        for any arena and is built before any graph capture) plus the stride-2 dgrad parity
         packs individually."""
-        specs = [sp for op in self.ops if hasattr(op, "pack_specs") for sp in op.pack_specs(rt.base)]
+        specs = [sp for op in self.ops if hasattr(op, "pack_specs") for sp in op.pack_specs()]
         key = tuple((w, dst) for _, w, dst, _ in specs)
         cache = self.__dict__.setdefault("_pack_tables", {})
         ent = cache.get(key)
@@ -562,9 +589,9 @@ class Plan:
                 cache.clear()
             ent = cache[key] = (table, len(jobs), singles)
         table, nj, singles = ent
-        L.call("yms_conv_pack_weights_batched", nj, table.data_ptr(), rt.st)
+        L.call("yms_conv_pack_weights_batched", nj, table.data_ptr(), rt.base, rt.st)
         for sp, w, dst, fd in singles:
-            L.call("yms_conv_pack_weight", sp, w, dst, fd, rt.st)
+            L.call("yms_conv_pack_weight", sp, w, rt.base + dst, fd, rt.st)
         rt.prepacked = True
 
     def new_arena(self, device, stream):

@@ -188,10 +188,17 @@ class _PlanFn(torch.autograd.Function):
             hook.begin(plan, pg, ptrs, views)
         for op in reversed(plan.ops):
             op.bwd(rt)
-            if hook is not None:
-                if rt.side is not None and hook.pending(op):
-                    rt.main.wait_stream(rt.side)   # the bucket's dw come from side-stream wgrads
-                hook.op_done(op)
+            if hook is not None and hook.pending(op):
+                if rt.side is not None:
+                    # the bucket's dw come from side-stream wgrads and its BN/bias grads from the main
+                    # stream: order the side stream after main and issue the collective from the side
+                    # stream, so the main stream never stalls on the wgrads (the collective's stream
+                    # waits on the side stream; finish() joins main to the collectives)
+                    rt.side.wait_stream(rt.main)
+                    with torch.cuda.stream(rt.side):
+                        hook.op_done(op)
+                else:
+                    hook.op_done(op)
         if rt.side is not None:
             rt.main.wait_stream(rt.side)
             rt.side = None
