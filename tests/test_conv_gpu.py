@@ -1,6 +1,7 @@
 """GPU parity of the implicit-GEMM convolution kernels (forward with every epilogue,
 dgrad, wgrad) against fp32 PyTorch-CPU convolution on the same dtype-rounded operands."""
 import ctypes
+import os
 
 import pytest
 import torch
@@ -172,3 +173,73 @@ def test_conv_bf16_large_tiles(shp):
     L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0, ws.data_ptr(),
            wsb, dw.data_ptr(), 0, L.stream_ptr())
     _close(dw.cpu(), wr.grad, 2e-3)
+
+
+# halo-tiled 3x3 stride-1 kernel (conv_halo.hip): reduction channels % 64 == 0.  Widths < 64 use
+# full-width tiles (TW = W), widths >= 64 with W % 16 == 0 use 16x16 tiles; the batch is one tall
+# virtual image with a zero separator row per image, so tiles straddle images.  Odd heights /
+# widths, several images per tile, cout not a multiple of 8 / 64 / 128, one and two column tiles.
+HALO = [
+    (3, 64, 7, 7, 64, 3, 1),
+    (2, 64, 20, 20, 80, 3, 1),
+    (5, 128, 9, 13, 40, 3, 1),
+    (2, 128, 40, 40, 128, 3, 1),
+    (1, 64, 48, 17, 72, 3, 1),
+    (2, 64, 64, 64, 64, 3, 1),
+    (1, 192, 16, 80, 136, 3, 1),
+    (2, 256, 20, 20, 256, 3, 1),
+    (1, 64, 3, 96, 64, 3, 1),
+]
+
+
+def test_conv_halo_paths_opt_in():
+    """The halo kernel is opt-in (YMS_HALO=1 is read once per process): run every HALO case in ONE
+    child interpreter with it enabled, so the default path and the halo path both run per session."""
+    import subprocess
+    import sys
+    env = dict(os.environ, YMS_HALO="1")
+    code = "import conftest\nimport test_conv_gpu as t\nfor s in t.HALO: t._halo_case(s)\nprint('halo ok', len(t.HALO))"
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                       cwd=os.path.dirname(os.path.abspath(__file__)))
+    assert r.returncode == 0 and "halo ok" in r.stdout, r.stdout[-3000:] + r.stderr[-3000:]
+
+
+def _halo_case(shp):
+    n, cin, h, w, cout, k, s = shp
+    dtype = torch.bfloat16
+    g = torch.Generator().manual_seed(hash(shp) % 997)
+    x = torch.randn(n, cin, h, w, generator=g)
+    wt = torch.randn(cout, cin, k, k, generator=g) / (cin * k * k) ** 0.5
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    z = ref_conv(x, wt, s, dtype)
+    # forward + BN statistics
+    y, st = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, stats=True)
+    _close(nchw(y, cout).cpu(), z, TOL["bf16"])
+    _close(st[:, 0, :cout].double().sum(0).cpu().float(), z.sum((0, 2, 3)), 1e-3)
+    _close(st[:, 1, :cout].double().sum(0).cpu().float(), (z * z).sum((0, 2, 3)), 1e-3)
+    if r8(cout) != cout:
+        assert y[..., cout:].abs().max().item() == 0
+    # forward with folded BN + SiLU + residual, output at a channel offset of a wider buffer
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh_ = torch.randn(cout, generator=g) * 0.1
+    res = torch.randn(n, cout, h, w, generator=g)
+    ya, _ = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, sc.cuda(), sh_.cuda(), L.ACT_SILU, nhwc(res, dtype),
+                     yld=r8(cout) + 16, yoff=8)
+    ref = F.silu(z * sc.view(1, -1, 1, 1) + sh_.view(1, -1, 1, 1)) + res.to(dtype).float()
+    _close(nchw(ya, cout, off=8).cpu(), ref, TOL["bf16"])
+    assert ya[..., :8].abs().max().item() == 0
+    # stride-1 dgrad (reduction over cout): store and accumulate
+    if cout % 64 == 0:
+        dz = torch.randn(n, cout, h, w, generator=g)
+        xr = x.to(dtype).float().requires_grad_(True)
+        F.conv2d(xr, wt.to(dtype).float(), None, 1, 1).backward(dz.to(dtype).float())
+        sp = ctypes.pointer(shp_)
+        wpt = pack(wt, shp_, dtype, 1)
+        dzb = nhwc(dz, dtype)
+        base = torch.randn(n, cin, h, w, generator=g)
+        for acc in (0, 1):
+            dx = nhwc(base, dtype)
+            L.call("yms_conv_dgrad", sp, dzb.data_ptr(), dzb.shape[-1], 0, wpt.data_ptr(), dx.data_ptr(),
+                   dx.shape[-1], 0, acc, L.stream_ptr())
+            exp = xr.grad + (base.to(dtype).float() if acc else 0)
+            _close(nchw(dx, cin).cpu(), exp, TOL["bf16"] * 2)

@@ -17,6 +17,9 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (64, 160, 160, 32, 32, 3, 1),
     (64, 20, 20, 256, 256, 3, 1),
     (64, 80, 80, 128, 80, 3, 1),
+    (64, 80, 80, 128, 64, 3, 1),
+    (64, 40, 40, 256, 64, 3, 1),
+    (64, 20, 20, 512, 80, 3, 1),
 ]
 dt = torch.bfloat16
 st = L.stream_ptr()

@@ -16,15 +16,10 @@
 // [32 pixels][cols] and read with ds_read_b64_tr_b16 (hardware transpose) so both
 // operands get 8 consecutive pixels per lane.  wgrad is split over pixels into fp32
 // partial slabs that a second kernel reduces deterministically (no atomics).
-#include "yms_common.hpp"
+#include "conv_common.hpp"
+#include "conv_halo.hpp"
 
 namespace yms {
-
-constexpr int NT_KCH = 8;     // 16-B chunks of K per k-tile row (128 B)
-constexpr int NT_ROWP = 144;  // LDS pitch: 128 B + 16 B pad (conflict-free ds_read_b128 over 16 rows)
-
-enum { MODE_FWD = 0, MODE_DGRAD = 1, MODE_DGRAD2 = 2 };  // DGRAD2: stride-2 dgrad by output parity
-enum { EPI_AFFINE = 0, EPI_STATS = 1, EPI_STORE = 2, EPI_ACCUM = 3 };
 
 struct NTParams {
   const char* src;
@@ -62,63 +57,6 @@ struct NTParams {
 // 16-B zero chunk: out-of-image / out-of-K im2col lanes load from here, so the A loads are
 // branch-free (no exec-masked regions around each global load).
 __device__ __attribute__((aligned(64))) u32x4 g_zero_chunk[4];
-
-// XCD-aware block order: hardware dispatches consecutive workgroup ids round-robin over the
-// 8 XCDs; remap (bijectively) so that consecutive LOGICAL ids -- the N tiles of one row
-// tile, and neighbouring row tiles that share im2col halo rows -- run on the same XCD and
-// share its L2 (MI355X_MICROARCH.md, Workgroup dispatch).
-__device__ __forceinline__ int xcd_remap(int orig, int nwg) {
-  const int q = nwg >> 3, r = nwg & 7, xcd = orig & 7, k = orig >> 3;
-  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + k;
-}
-
-template <typename T> struct Mfma;
-template <> struct Mfma<bf16> {
-  static __device__ __forceinline__ f32x16 mma(const u32x4& a, const u32x4& b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, a),
-                                                   __builtin_bit_cast(bf16x8, b), c, 0, 0, 0);
-  }
-};
-template <> struct Mfma<f16> {
-  static __device__ __forceinline__ f32x16 mma(const u32x4& a, const u32x4& b, f32x16 c) {
-    return __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8, a),
-                                                  __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
-  }
-};
-
-// s_waitcnt vmcnt(N) alone (expcnt/lgkmcnt left at their maxima), gfx9 encoding
-template <int N> __device__ __forceinline__ void wait_vmcnt() {
-  __builtin_amdgcn_s_waitcnt((N & 0xF) | (((N >> 4) & 3) << 14) | (0x7 << 4) | (0xF << 8));
-}
-// wait until at most min(n, MAXN) k-tiles of NG loads each are still in flight
-template <int NG, int MAXN> __device__ __forceinline__ void wait_tiles(int n) {
-  if constexpr (MAXN > 0) {
-    if (n >= MAXN) { wait_vmcnt<MAXN * NG>(); return; }
-    wait_tiles<NG, MAXN - 1>(n);
-  } else {
-    wait_vmcnt<0>();
-  }
-}
-// workgroup barrier that does NOT drain the vector-memory counter (so LDS-DMA loads of later
-// k-tiles stay in flight across it); the clobbers keep the compiler from moving LDS accesses
-// across it.
-__device__ __forceinline__ void raw_barrier() {
-  asm volatile("" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-}
-// raw-buffer LDS-DMA of 16 B per lane; an offset at or past the resource's num_records loads
-// zeros.  (The builtin is wrapped so the host pass of a kernel template never sees it: clang
-// silently drops the host stub of a template kernel that names it directly.)
-__device__ __forceinline__ void blds16(__amdgpu_buffer_rsrc_t r, char* lds_wave_base, uint32_t voff) {
-#if defined(__HIP_DEVICE_COMPILE__)
-  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (YMS_LDS void*)lds_wave_base, 16, voff, 0, 0, 0);
-#endif
-}
-__device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
-  __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g,
-                                   (void __attribute__((address_space(3)))*)lds_wave_base, 16, 0, 0);
-}
 
 // 16-bit types (GL): k-tiles are staged global->LDS directly with global_load_lds_dwordx4 into
 // an ST-deep ring of unpadded 128-B rows; 16-B chunk c of row r lives in slot
@@ -484,9 +422,6 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
 // 16-B row segments (+ residual / + accumulate in fp32).
 // ------------------------------------------------------------------------------------------
 constexpr int NTP_MAX_AFFINE_COLS = 512;   // wider affine outputs use conv_nt_kernel
-constexpr uint32_t NT_OOB = 0x80000000u;    // voffset past every A resource (num_records < 2^31)
-constexpr int NT_RSRC3 = 0x00020000;        // buffer descriptor word 3 (gfx9 raw buffer, 32-bit data)
-
 template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI, int OCC = 2>
 __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams p) {
   constexpr int NTHR = WGM * WGN * 64;
@@ -1275,16 +1210,7 @@ static TileChoice choose_tile(int ncols) {
   return TileChoice{0, 128};
 }
 
-static int cu_count() {
-  static int n = 0;
-  if (n == 0) {
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
-      n = 256;
-  }
-  return n;
-}
+static int cu_count() { return conv_cu_count(); }
 
 // persistent grid: at most two resident blocks per CU (the kernels are sized for 2/CU);
 // p.M is the largest parity class for DGRAD2
@@ -1455,6 +1381,17 @@ static void launch_wgrad(const TTParams& p, int var, int bm, int bn, dim3 grid, 
 
 }  // namespace yms
 
+int yms::conv_cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+  }
+  return n;
+}
+
 using namespace yms;
 
 extern "C" {
@@ -1532,6 +1469,8 @@ yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* p
 
 int yms_conv_stats_rows(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
+  HaloGeo hg;
+  if (conv_halo_geometry(s, 0, &hg)) return conv_halo_stats_rows(hg);
   TileChoice tc = choose_tile(s->cout);
   return rows_for(s->n * s->ho * s->wo, tc.cfg);
 }
@@ -1548,6 +1487,12 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   if (!view_ok(x_ld, x_off, s->cin) || !view_ok(y_ld, y_off, s->cout)) return YMS_ERR_INVALID;
   if (res && !view_ok(res_ld, res_off, s->cout)) return YMS_ERR_INVALID;
   const int es = elem_size(s->dtype);
+  {
+    HaloGeo hg;
+    if (conv_halo_geometry(s, 0, &hg))
+      return conv_halo_launch(s, 0, hg, x, x_ld, x_off, wpacked, y, y_ld, y_off, scale, shift, act, res, res_ld,
+                              res_off, stats, 0, (hipStream_t)stream);
+  }
   PackGeo g = pack_geo(s, 0);
   NTParams p{};
   p.src = (const char*)x;
@@ -1579,6 +1524,12 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
                           int accumulate, void* stream) {
   if (!shape_ok(s) || !dz || !wpacked_t || !dx) return YMS_ERR_INVALID;
   if (!view_ok(dz_ld, dz_off, s->cout) || !view_ok(dx_ld, dx_off, s->cin)) return YMS_ERR_INVALID;
+  {
+    HaloGeo hg;
+    if (conv_halo_geometry(s, 1, &hg))
+      return conv_halo_launch(s, 1, hg, dz, dz_ld, dz_off, wpacked_t, dx, dx_ld, dx_off, nullptr, nullptr, 0,
+                              nullptr, 0, 0, nullptr, accumulate, (hipStream_t)stream);
+  }
   NTParams p{};
   p.src = (const char*)dz;
   p.wp = (const char*)wpacked_t;
