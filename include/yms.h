@@ -176,6 +176,30 @@ yms_status yms_copy(void* dst, const void* src, size_t bytes, void* stream);
 /* y = cast(x) elementwise (fp32 <-> dtype), count elements. */
 yms_status yms_cast(int dtype_in, int dtype_out, long count, const void* x, void* y, void* stream);
 
+/* ---- depthwise k x k conv (YOLO-MS MS-Block inverted bottleneck) --------------- */
+/* groups = c, stride 1, pad k/2, k in {3,5,7,9}, c % 8 == 0; w: fp32 [c][k][k] (nn.Conv2d(groups=c)
+ * weight, used unpacked).  Not in the reference's code (annotations.md:66-133 diagram only). */
+typedef struct {
+  int n, h, w, c, k, dtype;
+} yms_dw_shape;
+/* rows of BN partial statistics written by yms_dwconv_fwd(stats != NULL): one per 8x32 tile */
+int yms_dwconv_stats_rows(const yms_dw_shape* s);
+/* stats == NULL: y = act(conv*scale + shift) (scale/shift NULL = identity); else y = conv (pre-BN
+ * z) and per-tile (sum z, sum z^2) rows [rows][2][stats_ld]. */
+yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
+                          int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
+                          int stats_ld, void* stream);
+/* dx (+)= depthwise conv of dz with the 180-degree rotated kernel */
+yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w, void* dx,
+                            int dx_ld, int dx_off, int accumulate, void* stream);
+/* dw[c][t] (+)= sum_pixels x(p + d_t) dz(p), fp32, via per-block partials in ws (deterministic) */
+size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s);
+yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
+                            int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream);
+/* y (+)= a + b over npix x c channels (b may be NULL); c % 8 == 0 */
+yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,
+                         int b_off, void* y, int y_ld, int y_off, int accumulate, void* stream);
+
 /* ---- head decode + NMS ------------------------------------------------------------------- */
 /* Raw head maps lvl[i]: NHWC [n, h_i, w_i, no_ld] with channels (64 DFL box logits, nc cls
  * logits).  out: [n, A, 4+nc] fp32 = (cx, cy, w, h)*stride_i, sigmoid(cls).  When nms_score

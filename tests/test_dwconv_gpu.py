@@ -1,0 +1,95 @@
+"""Depthwise k x k conv kernels (YOLO-MS MS-Block IB_k mid conv) through the C-ABI
+against fp32 PyTorch-CPU grouped convolution (groups = C) on the same dtype-rounded operands:
+forward (folded BN + SiLU, and BN statistics), dgrad (store / accumulate), wgrad; plus the
+branch-sum kernel yms_add_views.  Parity here is against torch's definition of a depthwise conv,
+not against the reference (which has no MS-Block code: annotations.md:66-133)."""
+import ctypes
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+from hiputil import DT, nchw, nhwc, r8
+from yms import _lib as L
+
+pytestmark = pytest.mark.gpu
+
+SHAPES = [(2, 20, 20, 64, 3), (1, 17, 33, 48, 5), (3, 40, 40, 32, 7), (2, 13, 9, 16, 9), (1, 80, 80, 64, 9),
+          (2, 8, 70, 40, 5)]
+TOL = {"f32": 2e-5, "bf16": 1e-2}
+
+
+def _close(got, ref, tol):
+    scale = ref.abs().max().item() + 1e-6
+    err = (got - ref).abs().max().item()
+    assert err <= tol * scale + 1e-6, f"max err {err:.3g} vs scale {scale:.3g} (tol {tol})"
+
+
+@pytest.mark.parametrize("dt", ["f32", "bf16"])
+@pytest.mark.parametrize("shp", SHAPES)
+def test_dwconv_fwd_dgrad_wgrad(shp, dt):
+    n, h, w, c, k = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(sum(shp))
+    x = torch.randn(n, c, h, w, generator=g)
+    wt = torch.randn(c, 1, k, k, generator=g) / k
+    xr = x.to(dtype).float()
+    z = F.conv2d(xr, wt, None, 1, k // 2, 1, c)
+    sh = L.DwShape(n, h, w, c, k, L.dtype_code(dtype))
+    sp = ctypes.pointer(sh)
+    st = L.stream_ptr()
+    wd = wt.contiguous().cuda()
+    xb = nhwc(x, dtype, ld=r8(c) + 8, off=8)
+    # eval: folded BN + SiLU, written at a channel offset
+    sc = torch.rand(c, generator=g) + 0.5
+    sf = torch.randn(c, generator=g) * 0.1
+    scd, sfd = sc.cuda(), sf.cuda()          # keep the device copies alive across the async launch
+    y = torch.zeros((n, h, w, r8(c) + 16), dtype=dtype, device="cuda")
+    L.call("yms_dwconv_fwd", sp, xb.data_ptr(), xb.shape[-1], 8, wd.data_ptr(), y.data_ptr(), y.shape[-1], 16,
+           scd.data_ptr(), sfd.data_ptr(), L.ACT_SILU, None, 0, st)
+    _close(nchw(y, c, off=16).cpu(), F.silu(z * sc.view(1, -1, 1, 1) + sf.view(1, -1, 1, 1)), TOL[dt])
+    assert y[..., :16].abs().max().item() == 0
+    # train: z + BN partial statistics
+    rows = L.lib().yms_dwconv_stats_rows(sp)
+    stt = torch.full((rows, 2, r8(c)), float("nan"), device="cuda")
+    y2 = torch.zeros((n, h, w, r8(c)), dtype=dtype, device="cuda")
+    L.call("yms_dwconv_fwd", sp, xb.data_ptr(), xb.shape[-1], 8, wd.data_ptr(), y2.data_ptr(), y2.shape[-1], 0,
+           None, None, 0, stt.data_ptr(), r8(c), st)
+    _close(nchw(y2, c).cpu(), z, TOL[dt])
+    s1 = stt[:, 0, :c].double().sum(0).cpu()
+    s2 = stt[:, 1, :c].double().sum(0).cpu()
+    _close(s1.float(), z.sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
+    _close(s2.float(), (z * z).sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
+    # backward
+    dz = torch.randn(n, c, h, w, generator=g)
+    xg = xr.clone().requires_grad_(True)
+    wg = wt.clone().requires_grad_(True)
+    F.conv2d(xg, wg, None, 1, k // 2, 1, c).backward(dz.to(dtype).float())
+    dzb = nhwc(dz, dtype)
+    base = torch.randn(n, c, h, w, generator=g)
+    for acc in (0, 1):
+        dx = nhwc(base, dtype)
+        L.call("yms_dwconv_dgrad", sp, dzb.data_ptr(), dzb.shape[-1], 0, wd.data_ptr(), dx.data_ptr(), dx.shape[-1], 0,
+               acc, st)
+        _close(nchw(dx, c).cpu(), xg.grad + (base.to(dtype).float() if acc else 0), TOL[dt] * 2)
+    wsb = L.lib().yms_dwconv_wgrad_ws_bytes(sp)
+    ws = torch.empty(wsb // 4, device="cuda")
+    dw = torch.full((c, 1, k, k), 0.5, device="cuda")
+    L.call("yms_dwconv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 8, dzb.data_ptr(), dzb.shape[-1], 0, ws.data_ptr(),
+           wsb, dw.data_ptr(), 1, st)
+    _close(dw.cpu() - 0.5, wg.grad, 1e-4 if dt == "f32" else 2e-3)
+
+
+def test_add_views():
+    g = torch.Generator().manual_seed(3)
+    a = torch.randn(2, 24, 5, 7, generator=g)
+    b = torch.randn(2, 24, 5, 7, generator=g)
+    ab = nhwc(a, torch.bfloat16, ld=40, off=8)
+    bb = nhwc(b, torch.bfloat16, ld=32, off=0)
+    y = nhwc(torch.ones(2, 24, 5, 7), torch.bfloat16, ld=24)
+    L.call("yms_add_views", L.BF16, 70, 24, ab.data_ptr(), 40, 8, bb.data_ptr(), 32, 0, y.data_ptr(), 24, 0, 1,
+           L.stream_ptr())
+    ref = a.to(torch.bfloat16).float() + b.to(torch.bfloat16).float() + 1
+    _close(nchw(y, 24).cpu(), ref, 1e-2)
+    L.call("yms_add_views", L.BF16, 70, 24, ab.data_ptr(), 40, 8, None, 0, 0, y.data_ptr(), 24, 0, 0, L.stream_ptr())
+    assert torch.equal(nchw(y, 24).cpu(), a.to(torch.bfloat16).float())

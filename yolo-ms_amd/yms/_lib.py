@@ -33,6 +33,10 @@ class ConvShape(ctypes.Structure):
                 ("n", "h", "w", "cin", "cout", "k", "stride", "pad", "ho", "wo", "dtype")]
 
 
+class DwShape(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_int) for k in ("n", "h", "w", "c", "k", "dtype")]
+
+
 class PackJob(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("packed", ctypes.c_void_p)] + [
         (k, ctypes.c_int) for k in ("cout", "cin", "ks", "rows", "kp_elems", "c8_in", "for_dgrad", "dtype")]
@@ -45,6 +49,7 @@ _F = ctypes.c_float
 _D = ctypes.c_double
 _SZ = ctypes.c_size_t
 _SP = ctypes.POINTER(ConvShape)
+_DP = ctypes.POINTER(DwShape)
 
 _SIGS = {
     "yms_version": (ctypes.c_char_p, []),
@@ -81,6 +86,12 @@ _SIGS = {
     "yms_cast": (_I, [_I, _I, _L, _P, _P, _P]),
     "yms_zero": (_I, [_P, _SZ, _P]),
     "yms_copy": (_I, [_P, _P, _SZ, _P]),
+    "yms_dwconv_stats_rows": (_I, [_DP]),
+    "yms_dwconv_fwd": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
+    "yms_dwconv_dgrad": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
+    "yms_dwconv_wgrad_ws_bytes": (_SZ, [_DP]),
+    "yms_dwconv_wgrad": (_I, [_DP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
+    "yms_add_views": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P]),
     "yms_head_decode": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P]),
     "yms_dfl": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "yms_nms_prep": (_I, [_I, _I, _I, _P, _F, _P, _P, _P, _P]),
