@@ -163,9 +163,17 @@ def cpu_threads():
     return n
 
 
+def _oracle(version):
+    if version.startswith("ms-"):
+        from oracle import ms_ref as M
+    else:
+        from oracle import model_ref as M
+    return M
+
+
 def cpu_baseline_train(version, nc, size, batch=8, steps=8):
     """Oracle (fp32 torch-CPU restatement of the reference graph) train step on host cores."""
-    from oracle import model_ref as M
+    M = _oracle(version)
     threads = cpu_threads()
     sd = M.init_params(version, nc)
     p = {k: (t.clone().requires_grad_(True) if t.is_floating_point() and "running" not in k
@@ -192,8 +200,8 @@ def cpu_baseline_train(version, nc, size, batch=8, steps=8):
 
 
 def cpu_baseline_infer(version, nc, size, batch=8, steps=12):
-    from oracle import model_ref as M
     from oracle import nms as onms
+    M = _oracle(version)
     sd = M.init_params(version, nc)
     x = torch.randn(batch, 3, size, size, generator=torch.Generator().manual_seed(0))
     threads = cpu_threads()
@@ -309,18 +317,30 @@ def main():
 
     if rank == 0:
         from oracle import model_ref as M
-        flops_img = M.count_conv_flops(a.version, a.nc, a.size, a.size)
+        if a.version.startswith("ms-"):
+            # YOLO-MS family: dense conv FLOPs from the plan (the depthwise k x k FLOPs are VALU work
+            # and are reported separately, outside the MFMA conv roofline)
+            from yms import runner as _r
+            _m = YOLOv8(a.version, a.nc).train()
+            _p = _r.get_plan(_m, [torch.empty(1, 3, a.size, a.size, device="meta")], dtype, True)
+            flops_img = _p.flops
+            dw_flops_img = sum(getattr(op, "dw_flops", 0) for op in _p.ops)
+        else:
+            flops_img = M.count_conv_flops(a.version, a.nc, a.size, a.size)
+            dw_flops_img = 0
         line = {"metric": "images/sec (train+infer) YOLO-MS-S 640x640 bf16 at 1/2/4/8 MI355X; mAP parity",
                 "unit": "images/sec", "n_gpus": world, "steps": a.steps, "warmup": a.warmup,
                 "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": a.dtype,
-                "data": f"synthetic (randn images, torch-default random-init weights of the YOLOv8-{a.version} graph)"}
+                "data": f"synthetic (randn images, torch-default random-init weights of the "
+                        f"{'YOLO-MS ' + a.version if a.version.startswith('ms-') else 'YOLOv8-' + a.version} graph)"}
         if "train" in result:
             tr = result["train"]
             line["value"] = round(tr["img_s"], 2)
             line["ms_per_step"] = round(tr["dt"] / a.steps * 1e3, 3)
             line["ms_per_step_median"] = round(tr["med_ms"], 3)
-            tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L"}.get(
-                a.version, f"custom: YOLO-MS-{a.version.upper()}")
+            tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L",
+                    "ms-l": "configs[3]: YOLO-MS-L (MS-Block / HKS 3-5-7-9 depthwise graph)",
+                    "ms-s": "YOLO-MS-S (MS-Block / HKS graph)"}.get(a.version, f"custom: YOLO-MS-{a.version.upper()}")
             line["config"] = {"workload": f"{tcfg} (reference YOLOv8-'{a.version}' graph) "
                                           f"{a.size}x{a.size} {a.dtype} training, B={a.batch}/GPU, fwd+loss+bwd+"
                                           "allreduce+SGD-nesterov step",
@@ -329,6 +349,7 @@ def main():
                               "loss": "surrogate sum(mean(o^2)) over the 3 head maps (reference loss "
                                       "crashes for nc=80, SURVEY 0.5)",
                               "conv_gflop_per_img_fwd": round(flops_img / 1e9, 3),
+                              "depthwise_gflop_per_img_fwd": round(dw_flops_img / 1e9, 3),
                               "peak_hbm_gib": round(tr["peak_gb"], 2),
                               "hip_graph": tr["graph"]}
             if "train_prof" in result:

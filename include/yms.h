@@ -80,13 +80,14 @@ yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* pack
 yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* dst_base, void* stream);
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------------------- */
-/* Number of fp32 rows of BN partial statistics written by yms_conv_fwd(stats != NULL);
- * the stats workspace is [rows][2][stats_ld] floats, stats_ld = yms_conv_stats_ld(). */
+/* Number of fp32 rows of BN partial statistics written by yms_conv_fwd(stats != NULL): one per
+ * 128 output pixels (ceil(n*ho*wo / 128)); the stats workspace is [rows][2][stats_ld] floats,
+ * stats_ld = yms_conv_stats_ld(). */
 int yms_conv_stats_rows(const yms_conv_shape* s);
 int yms_conv_stats_ld(const yms_conv_shape* s);
 /* Forward.  stats == NULL: y = act(conv(x)*scale[c] + shift[c]) (+ res) (scale/shift may
- * be NULL = identity).  stats != NULL (training): y = conv(x) (pre-BN z) and per-tile
- * partial sums (sum z, sum z^2) into stats. */
+ * be NULL = identity).  stats != NULL (training): y = conv(x) (pre-BN z) and per-128-pixel
+ * rows (sum z, sum (z - row mean)^2) into stats. */
 yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
                         const void* wpacked, void* y, int y_ld, int y_off,
                         const float* scale, const float* shift, int act,
@@ -105,10 +106,13 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
 /* Eval: scale = g/sqrt(rv+eps), shift = b - rm*scale (bias-only conv: g=NULL -> scale 1, shift b). */
 yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float* rmean,
                        const float* rvar, float eps, float* scale, float* shift, void* stream);
-/* Train: reduce partial stats of `count` pixels -> mean/invstd, scale/shift, and update the
+/* Train: merge the statistics rows of `count` pixels -> mean/invstd, scale/shift, and update the
  * running buffers (unbiased var, momentum) exactly like nn.BatchNorm2d.  mean_invstd: [2][c].
+ * Row r = (sum z, sum (z - mean_r)^2) over n_r pixels: n_r = row_counts[r] when row_counts is
+ * given (yms_dwconv_stats_counts), else min(128, count - 128 r) (the convolutions' rows, which
+ * requires 128 (rows - 1) < count <= 128 rows).  Rows are merged with Chan's update in fp64.
  * The stats table is consumed: long tables are pre-reduced in place. */
-yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count, const float* row_counts,
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream);
@@ -184,8 +188,11 @@ typedef struct {
 } yms_dw_shape;
 /* rows of BN partial statistics written by yms_dwconv_fwd(stats != NULL): one per 8x32 tile */
 int yms_dwconv_stats_rows(const yms_dw_shape* s);
+/* host: pixels of each statistics row (the tile's in-image extent) -> counts[rows], for
+ * yms_bn_finalize's row_counts */
+yms_status yms_dwconv_stats_counts(const yms_dw_shape* s, float* counts);
 /* stats == NULL: y = act(conv*scale + shift) (scale/shift NULL = identity); else y = conv (pre-BN
- * z) and per-tile (sum z, sum z^2) rows [rows][2][stats_ld]. */
+ * z) and per-tile (sum z, sum (z - tile mean)^2) rows [rows][2][stats_ld]. */
 yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
                           int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
                           int stats_ld, void* stream);
@@ -199,6 +206,20 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
 /* y (+)= a + b over npix x c channels (b may be NULL); c % 8 == 0 */
 yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,
                          int b_off, void* y, int y_ld, int y_off, int accumulate, void* stream);
+
+/* ---- mAP@0.5 evaluation (validate_epoch's torchmetrics call, train.py:41-47,146,152-153) ---- */
+/* GPU: per image (det_off / gt_off prefix offsets, n_images + 1 entries), rank every detection in
+ * its class (stable, score descending), keep the first 100, and greedily match them to the
+ * image's ground truths at IoU >= 0.5 (COCOeval semantics) -> tp[d], kept[d] flags.
+ * rank_ws: n_det ints of scratch.  max_gt_per_image <= 2048. */
+yms_status yms_map_match(int n_images, const float* det_boxes, const float* det_scores, const int* det_labels,
+                         const int* det_off, const float* gt_boxes, const int* gt_labels, const int* gt_off,
+                         uint8_t* tp, uint8_t* kept, int* rank_ws, int max_gt_per_image, void* stream);
+/* HOST (not stream-ordered; host arrays): COCOeval.accumulate at one IoU threshold -> per-class
+ * AP (-1 for classes without ground truth) and their mean. */
+yms_status yms_map_accumulate(int n_det, const float* scores, const int* labels, const int* image,
+                              const uint8_t* tp, const uint8_t* kept, int n_classes, const int* n_gt,
+                              double* ap, double* map);
 
 /* ---- head decode + NMS ------------------------------------------------------------------- */
 /* Raw head maps lvl[i]: NHWC [n, h_i, w_i, no_ld] with channels (64 DFL box logits, nc cls

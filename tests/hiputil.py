@@ -56,6 +56,32 @@ def conv_fwd(xb, w, sh, dtype, scale=None, shift=None, act=0, res=None, stats=Fa
     return y, st
 
 
+def merge_moments(st, c, npix, counts=None):
+    """BN statistics rows [rows][2][ld] (sum z, sum (z - row mean)^2 over n_r pixels; n_r = counts or
+    the 128-pixel rule) -> (sum z, M2 about the global mean) per channel, fp64 on the host."""
+    st = st.double().cpu()
+    rows = st.shape[0]
+    if counts is None:
+        counts = torch.clamp(npix - 128 * torch.arange(rows, dtype=torch.float64), max=128.0)
+    n = torch.as_tensor(counts, dtype=torch.float64).cpu().view(-1, 1)
+    s1, m2 = st[:, 0, :c], st[:, 1, :c]
+    mean = s1.sum(0) / npix
+    return s1.sum(0), (m2 + n * (s1 / n - mean) ** 2).sum(0)
+
+
+def check_moments(st, z, tol, counts=None):
+    """Statistics rows of the pre-BN tensor z (NCHW fp32) against its exact sum and centred M2."""
+    c = z.shape[1]
+    npix = z.numel() // c
+    s1, m2 = merge_moments(st, c, npix, counts)
+    zd = z.double()
+    ref1 = zd.sum((0, 2, 3))
+    ref2 = ((zd - zd.mean((0, 2, 3), keepdim=True)) ** 2).sum((0, 2, 3))
+    e1 = ((s1 - ref1).abs().max() / (ref1.abs().max() + 1e-6)).item()
+    e2 = ((m2 - ref2).abs() / ref2.clamp_min(1e-30)).max().item()
+    assert e1 <= tol and e2 <= tol, (e1, e2)
+
+
 def ref_conv(x, w, s, dtype):
     """fp32 conv on operands rounded to `dtype` (what the MFMA path multiplies)."""
     xr = x.to(dtype).float()

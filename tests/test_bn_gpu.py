@@ -95,3 +95,56 @@ def test_bias_bwd_fused():
         torch.cuda.synchronize()
         assert ((db.double().cpu() - ref).abs().max() / ref.abs().max()).item() < 1e-5
         assert int(cnt[0]) == 0
+
+
+def _finalize(st, c, npix, counts=None):
+    gam = torch.rand(c, generator=torch.Generator().manual_seed(c)).cuda() + 0.5
+    bet = torch.randn(c, generator=torch.Generator().manual_seed(c + 1)).cuda()
+    rm, rv = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
+    mi = torch.empty(2 * c, device="cuda")
+    sc, sh = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
+    L.call("yms_bn_finalize", c, st.data_ptr(), st.shape[0], st.shape[2], npix, L.ptr(counts), gam.data_ptr(),
+           bet.data_ptr(), rm.data_ptr(), rv.data_ptr(), ctypes.c_float(0.03), ctypes.c_float(1e-3), mi.data_ptr(),
+           sc.data_ptr(), sh.data_ptr(), L.stream_ptr())
+    torch.cuda.synchronize()
+    return mi[:c].double().cpu(), mi[c:].double().cpu(), rv.double().cpu()
+
+
+@pytest.mark.parametrize("b,h,w,offset", [(2, 3, 2, 300.0), (4, 40, 40, 1000.0), (9, 80, 80, 50.0)])
+def test_bn_stats_large_mean_conv_and_dw(b, h, w, offset):
+    """Training BN statistics where |mean| / std ~ 4e2-8e3 (sum z^2 - n mean^2 in fp32 would lose
+    every digit): conv (128-pixel rows; > 256 rows exercises the in-place pre-reduction) and
+    depthwise (8x32 tile rows with a row-count table) against fp64 moments of the kernels' own
+    fp32 z, through yms_bn_finalize."""
+    from hiputil import conv_fwd, nchw, nhwc, shape, r8
+    c = 64
+    g = torch.Generator().manual_seed(b * h)
+    x = offset + torch.randn(b, c, h, w, generator=g)
+    wt = (torch.rand(c, c, 1, 1, generator=g) + 0.5) / c
+    sp = shape(b, h, w, c, c, 1, 1, torch.float32)
+    y, st = conv_fwd(nhwc(x, torch.float32), wt, sp, torch.float32, stats=True)
+    z = nchw(y, c).double().cpu()
+    mean, istd, rv = _finalize(st, c, b * h * w)
+    var = z.var((0, 2, 3), unbiased=False)
+    assert ((mean - z.mean((0, 2, 3))).abs() / z.mean((0, 2, 3)).abs()).max().item() < 1e-6
+    assert ((istd - 1 / (var + 1e-3).sqrt()).abs() * (var + 1e-3).sqrt()).max().item() < 1e-4
+    n = b * h * w
+    assert ((rv - (0.97 + 0.03 * var * n / (n - 1))).abs() / rv).max().item() < 1e-5
+    # depthwise 3x3 on the same large-offset input
+    ds = L.DwShape(b, h, w, c, 3, L.F32)
+    dsp = ctypes.pointer(ds)
+    wd = (torch.rand(c, 1, 3, 3, generator=g) + 0.5).cuda() / 9
+    rows = L.lib().yms_dwconv_stats_rows(dsp)
+    sd = torch.full((rows, 2, r8(c)), float("nan"), device="cuda")
+    counts = torch.empty(rows)
+    L.call("yms_dwconv_stats_counts", dsp, counts.data_ptr())
+    assert counts.sum().item() == n
+    xb = nhwc(x, torch.float32)
+    yd = torch.zeros((b, h, w, r8(c)), device="cuda")
+    L.call("yms_dwconv_fwd", dsp, xb.data_ptr(), xb.shape[-1], 0, wd.data_ptr(), yd.data_ptr(), yd.shape[-1], 0,
+           None, None, 0, sd.data_ptr(), r8(c), L.stream_ptr())
+    zd = nchw(yd, c).double().cpu()
+    mean, istd, _ = _finalize(sd, c, n, counts.cuda())
+    var = zd.var((0, 2, 3), unbiased=False)
+    assert ((mean - zd.mean((0, 2, 3))).abs() / zd.mean((0, 2, 3)).abs()).max().item() < 1e-6
+    assert ((istd - 1 / (var + 1e-3).sqrt()).abs() * (var + 1e-3).sqrt()).max().item() < 1e-4

@@ -7,7 +7,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from hiputil import DT, conv_fwd, nchw, nhwc, pack, r8, ref_conv, shape
+from hiputil import DT, check_moments, conv_fwd, nchw, nhwc, pack, r8, ref_conv, shape
 from yms import _lib as L
 
 pytestmark = pytest.mark.gpu
@@ -68,10 +68,7 @@ def test_conv_fwd_stats(shp, dt):
     y, st = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, stats=True)
     z = ref_conv(x, wt, s, dtype)
     _close(nchw(y, cout).cpu(), z, TOL[dt])
-    s1 = st[:, 0, :cout].double().sum(0).cpu()
-    s2 = st[:, 1, :cout].double().sum(0).cpu()
-    _close(s1.float(), z.sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
-    _close(s2.float(), (z * z).sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
+    check_moments(st, z, 1e-4 if dt == "f32" else 1e-3)
 
 
 def test_conv_fwd_channel_offsets():
@@ -149,8 +146,7 @@ def test_conv_bf16_large_tiles(shp):
     y, st = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, stats=True)
     z = ref_conv(x, wt, s, dtype)
     _close(nchw(y, cout).cpu(), z, TOL["bf16"])
-    _close(st[:, 0, :cout].double().sum(0).cpu().float(), z.sum((0, 2, 3)), 1e-3)
-    _close(st[:, 1, :cout].double().sum(0).cpu().float(), (z * z).sum((0, 2, 3)), 1e-3)
+    check_moments(st, z, 1e-3)
     sc = torch.rand(cout, generator=g) + 0.5
     sh_ = torch.randn(cout, generator=g) * 0.1
     ya, _ = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, sc.cuda(), sh_.cuda(), L.ACT_SILU)
@@ -215,8 +211,7 @@ def _halo_case(shp):
     # forward + BN statistics
     y, st = conv_fwd(nhwc(x, dtype), wt, shp_, dtype, stats=True)
     _close(nchw(y, cout).cpu(), z, TOL["bf16"])
-    _close(st[:, 0, :cout].double().sum(0).cpu().float(), z.sum((0, 2, 3)), 1e-3)
-    _close(st[:, 1, :cout].double().sum(0).cpu().float(), (z * z).sum((0, 2, 3)), 1e-3)
+    check_moments(st, z, 1e-3)
     if r8(cout) != cout:
         assert y[..., cout:].abs().max().item() == 0
     # forward with folded BN + SiLU + residual, output at a channel offset of a wider buffer

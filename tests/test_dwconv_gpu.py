@@ -1,6 +1,6 @@
 """Depthwise k x k conv kernels (YOLO-MS MS-Block IB_k mid conv) through the C-ABI
 against fp32 PyTorch-CPU grouped convolution (groups = C) on the same dtype-rounded operands:
-forward (folded BN + SiLU, and BN statistics), dgrad (store / accumulate), wgrad; plus the
+forward (folded BN + SiLU, and BN statistics: per-tile sum and centred M2), dgrad (store / accumulate), wgrad; plus the
 branch-sum kernel yms_add_views.  Parity here is against torch's definition of a depthwise conv,
 not against the reference (which has no MS-Block code: annotations.md:66-133)."""
 import ctypes
@@ -9,7 +9,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from hiputil import DT, nchw, nhwc, r8
+from hiputil import DT, check_moments, nchw, nhwc, r8
 from yms import _lib as L
 
 pytestmark = pytest.mark.gpu
@@ -56,10 +56,10 @@ def test_dwconv_fwd_dgrad_wgrad(shp, dt):
     L.call("yms_dwconv_fwd", sp, xb.data_ptr(), xb.shape[-1], 8, wd.data_ptr(), y2.data_ptr(), y2.shape[-1], 0,
            None, None, 0, stt.data_ptr(), r8(c), st)
     _close(nchw(y2, c).cpu(), z, TOL[dt])
-    s1 = stt[:, 0, :c].double().sum(0).cpu()
-    s2 = stt[:, 1, :c].double().sum(0).cpu()
-    _close(s1.float(), z.sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
-    _close(s2.float(), (z * z).sum((0, 2, 3)), 1e-4 if dt == "f32" else 1e-3)
+    counts = torch.empty(rows)
+    L.call("yms_dwconv_stats_counts", sp, counts.data_ptr())
+    assert counts.sum().item() == n * h * w
+    check_moments(stt, z, 1e-4 if dt == "f32" else 1e-3, counts)
     # backward
     dz = torch.randn(n, c, h, w, generator=g)
     xg = xr.clone().requires_grad_(True)

@@ -38,73 +38,96 @@ __global__ void bn_fold_kernel(int c, const float* g, const float* b, const floa
   shift[i] = b[i] - rm[i] * sc;
 }
 
-// stats: [rows][2][ld]; 32 channels x 32 row-lanes per block (1024 threads), 4 independent
-// fp64 accumulators per lane so the row loop is load-throughput, not latency, bound.
-// Pre-reduction for long statistics tables (one row per conv M tile): block (cb, s) sums rows
-// [s*R, (s+1)*R) of channels [64cb, 64cb+64) in fp64 and stores the sum over row s*R -- the
-// first row of its own range, so no block reads a row another block writes.
-__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int c, float* stats, int rows, int ld, int R) {
-  __shared__ double red[2][4][64];
+// Statistics rows (conv_common.hpp contract): row r = (sum z, sum (z - mean_r)^2) over n_r
+// pixels, n_r = counts[r] when a count table is given (depthwise tiles), else the 128-pixel
+// rule min(128, count - 128 r) of the NT convolutions.  Rows are merged with Chan's pairwise
+// update, M2 = sum_r [M2_r + n_r (mean_r - mean)^2], in fp64 -- no sum z^2 - n mean^2
+// cancellation anywhere.
+__device__ __forceinline__ double stats_row_n(int r, const float* counts, long count) {
+  return counts ? (double)counts[r] : (double)min(128l, count - 128l * r);
+}
+
+// Pre-reduction for long statistics tables: block (cb, s) merges rows [s*R, (s+1)*R) of
+// channels [64cb, 64cb+64) and stores the merged (sum, M2) over row s*R -- the first row of its
+// own range, so no block reads a row another block writes.  256 threads = 64 channels x 4 lanes.
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int c, float* stats, int rows, int ld, int R,
+                                                               const float* counts, long count) {
+  __shared__ double red[3][4][64];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + tx;
   const int r0 = blockIdx.y * R, r1 = min(rows, r0 + R);
-  double a1 = 0.0, a2 = 0.0, b1 = 0.0, b2 = 0.0;
-  if (ch < c) {
-    int r = r0 + ty;
-    for (; r + 4 < r1; r += 8) {
+  double a1 = 0.0, an = 0.0;
+  if (ch < c)
+    for (int r = r0 + ty; r < r1; r += 4) {
       a1 += stats[(long)r * 2 * ld + ch];
-      a2 += stats[(long)r * 2 * ld + ld + ch];
-      b1 += stats[(long)(r + 4) * 2 * ld + ch];
-      b2 += stats[(long)(r + 4) * 2 * ld + ld + ch];
+      an += stats_row_n(r, counts, count);
     }
-    if (r < r1) {
-      a1 += stats[(long)r * 2 * ld + ch];
-      a2 += stats[(long)r * 2 * ld + ld + ch];
+  red[0][ty][tx] = a1;
+  red[1][ty][tx] = an;
+  __syncthreads();
+  const double t1 = (red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]);
+  const double tn = (red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]);
+  const double mu = tn > 0.0 ? t1 / tn : 0.0;
+  double a2 = 0.0;
+  if (ch < c)
+    for (int r = r0 + ty; r < r1; r += 4) {
+      const double n = stats_row_n(r, counts, count);
+      const double d = (double)stats[(long)r * 2 * ld + ch] / n - mu;
+      a2 += (double)stats[(long)r * 2 * ld + ld + ch] + n * d * d;
     }
-  }
-  red[0][ty][tx] = a1 + b1;
-  red[1][ty][tx] = a2 + b2;
+  red[2][ty][tx] = a2;
   __syncthreads();
   if (ty == 0 && ch < c) {
-    const double t1 = (red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]);
-    const double t2 = (red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]);
+    const double t2 = (red[2][0][tx] + red[2][1][tx]) + (red[2][2][tx] + red[2][3][tx]);
     stats[(long)r0 * 2 * ld + ch] = (float)t1;
     stats[(long)r0 * 2 * ld + ld + ch] = (float)t2;
   }
 }
 
-// rows are read at stride rs (rs > 1 after bn_stats_partial_kernel)
+// pixels of merged row k (rows [k*rs, min(rows_total, (k+1)*rs)) of the original table)
+__device__ __forceinline__ double merged_row_n(int k, int rs, int rows_total, const float* counts, long count) {
+  if (!counts) return (double)min((long)rs * 128l, count - (long)k * rs * 128l);
+  double n = 0.0;
+  for (int r = k * rs, e = min(rows_total, (k + 1) * rs); r < e; ++r) n += (double)counts[r];
+  return n;
+}
+
+// rows are read at stride rs (rs > 1 after bn_stats_partial_kernel); 32 channels x 32 row-lanes
+// per block (1024 threads); two passes: the mean from the row sums, then the merged M2
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* stats, int rows, int ld, int rs,
-                                                           long count, const float* g, const float* b,
-                                                           float* rm, float* rv, float momentum, float eps,
-                                                           float* mi, float* scale, float* shift) {
-  __shared__ double red[2][32][33];
+                                                           int rows_total, const float* counts, long count,
+                                                           const float* g, const float* b, float* rm, float* rv,
+                                                           float momentum, float eps, float* mi, float* scale,
+                                                           float* shift) {
+  __shared__ double red[32][33];
+  __shared__ double mean_s[32];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int ch = blockIdx.x * 32 + tx;
-  double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
-  if (ch < c) {
-    int r = ty;
-    for (; r + 96 < rows; r += 128) {
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        a1[u] += stats[(long)(r + 32 * u) * rs * 2 * ld + ch];
-        a2[u] += stats[(long)(r + 32 * u) * rs * 2 * ld + ld + ch];
-      }
-    }
-    for (; r < rows; r += 32) {
-      a1[0] += stats[(long)r * rs * 2 * ld + ch];
-      a2[0] += stats[(long)r * rs * 2 * ld + ld + ch];
-    }
+  double a1 = 0.0;
+  if (ch < c)
+    for (int r = ty; r < rows; r += 32) a1 += stats[(long)r * rs * 2 * ld + ch];
+  red[ty][tx] = a1;
+  __syncthreads();
+  if (ty == 0) {
+    double t1 = 0.0;
+    for (int k = 0; k < 32; ++k) t1 += red[k][tx];
+    mean_s[tx] = t1 / (double)count;
   }
-  red[0][ty][tx] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-  red[1][ty][tx] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+  __syncthreads();
+  const double mean = mean_s[tx];
+  double a2 = 0.0;
+  if (ch < c)
+    for (int r = ty; r < rows; r += 32) {
+      const double n = merged_row_n(r, rs, rows_total, counts, count);
+      const double d = (double)stats[(long)r * rs * 2 * ld + ch] / n - mean;
+      a2 += (double)stats[(long)r * rs * 2 * ld + ld + ch] + n * d * d;
+    }
+  red[ty][tx] = a2;   // pass-1 partials were consumed before the barrier above
   __syncthreads();
   if (ty == 0 && ch < c) {
-    double t1 = 0.0, t2 = 0.0;
-    for (int k = 0; k < 32; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
-    const double mean = t1 / (double)count;
-    double var = t2 / (double)count - mean * mean;
-    if (var < 0.0) var = 0.0;
+    double t2 = 0.0;
+    for (int k = 0; k < 32; ++k) t2 += red[k][tx];
+    const double var = t2 / (double)count;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const double uvar = count > 1 ? var * (double)count / (double)(count - 1) : var;
     if (rm) rm[ch] = (float)((1.0 - momentum) * (double)rm[ch] + momentum * mean);
@@ -707,24 +730,25 @@ yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float
   return launch_status();
 }
 
-yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count, const float* row_counts,
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream) {
   if (c <= 0 || !stats || rows <= 0 || count <= 0 || !gamma || !beta || !mean_invstd || !scale || !shift)
     return YMS_ERR_INVALID;
   if (stats_ld < c) return YMS_ERR_INVALID;
+  if (!row_counts && (count > 128l * rows || count <= 128l * (rows - 1))) return YMS_ERR_INVALID;
   int rs = 1, nrows = rows;
   if (rows > 256) {   // long tables: pre-reduce in parallel (in place), then finalize the partial rows
     const int S = std::min(256, cdiv(rows, 64));
     rs = cdiv(rows, S);
     nrows = cdiv(rows, rs);
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(cdiv(c, 64), nrows), dim3(256), 0, (hipStream_t)stream, c,
-                       stats, rows, stats_ld, rs);
+                       stats, rows, stats_ld, rs, row_counts, count);
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c,
-                     (const float*)stats, nrows, stats_ld, rs, count, gamma, beta, rmean, rvar, momentum, eps,
-                     mean_invstd, scale, shift);
+                     (const float*)stats, nrows, stats_ld, rs, rows, row_counts, count, gamma, beta, rmean, rvar,
+                     momentum, eps, mean_invstd, scale, shift);
   return launch_status();
 }
 

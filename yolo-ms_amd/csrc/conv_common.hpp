@@ -72,6 +72,64 @@ __device__ __forceinline__ void glds16(const void* g, char* lds_wave_base) {
 constexpr uint32_t NT_OOB = 0x80000000u;    // voffset past every A resource (num_records < 2^31)
 constexpr int NT_RSRC3 = 0x00020000;        // buffer descriptor word 3 (gfx9 raw buffer, 32-bit data)
 
+// ------------------------------------------------------------------------------------------
+// BN training statistics contract (consumed by yms_bn_finalize, bn_pool.hip): one row per
+// 128 output pixels (row r covers pixels [128r, min(128r + 128, M))), row[0][c] = sum of z,
+// row[1][c] = sum of (z - mean_r)^2 about that row's OWN mean.  Centred second moments keep
+// the variance exact to fp32 rounding however large |mean| / std is (sum z^2 - n mean^2 loses
+// (mean/std)^2 x eps relative precision, which the deep MS-Block graphs amplify).
+// ------------------------------------------------------------------------------------------
+// One wave's 32-column MFMA block (TM tiles of 32 rows; accumulator i of lane half lh is row
+// a*32 + (i&3) + 8*(i>>2) + 4*lh): sum and centred M2 over its first nw rows, two passes over
+// the registers, combined across the two lane halves.
+template <int TM, typename Acc>
+__device__ __forceinline__ void wave_col_moments(const Acc& acc, int b, int nw, int lh, float& s1, float& m2) {
+  const bool full = nw >= TM * 32;
+  float s = 0.f;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (full || a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh < nw) s += acc[a][b][i];
+  s += __shfl_xor(s, 32);
+  const float mu = nw > 0 ? s / (float)nw : 0.f;
+  float q = 0.f;
+#pragma unroll
+  for (int a = 0; a < TM; ++a)
+#pragma unroll
+    for (int i = 0; i < 16; ++i)
+      if (full || a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh < nw) {
+        const float d = acc[a][b][i] - mu;
+        q += d * d;
+      }
+  q += __shfl_xor(q, 32);
+  s1 = s;
+  m2 = q;
+}
+
+// Chan merge of NP consecutive row groups of R rows each (group w: sum s[w*stride], M2
+// m[w*stride]); only the first nrows rows exist.  -> sum and M2 about the merged mean.
+template <int NP, int R>
+__device__ __forceinline__ void merge_moments(const float* s, const float* m, int stride, int nrows, float& t1,
+                                              float& t2) {
+  nrows = min(nrows, NP * R);
+  float tot = 0.f;
+#pragma unroll
+  for (int w = 0; w < NP; ++w) tot += s[w * stride];
+  const float mu = nrows > 0 ? tot / (float)nrows : 0.f;
+  float q = 0.f;
+#pragma unroll
+  for (int w = 0; w < NP; ++w) {
+    const int nw = min(R, max(0, nrows - w * R));
+    if (nw > 0) {
+      const float d = s[w * stride] / (float)nw - mu;
+      q += m[w * stride] + (float)nw * d * d;
+    }
+  }
+  t1 = tot;
+  t2 = q;
+}
+
 
 // host: CU count of the current device (persistent grids)
 int conv_cu_count();

@@ -16,7 +16,8 @@
 // k-tiles (tap t, chunk group cg) and a double-buffered halo.  The halo of chunk-step j+1 is
 // issued in pieces alongside the weight loads of taps 0..HS-1 of chunk-step j, so every wave
 // issues a fixed, tap-determined number of DMAs per step and waits with a counted vmcnt.
-// Separator / padding / dead rows of a tile are masked out of the BN statistics and not stored.
+// Separator / padding / dead rows of a tile are not stored.  Training-forward convolutions with BN
+// statistics always take the NT kernels (their per-128-pixel statistics rows, conv_common.hpp).
 #include <algorithm>
 #include <cstdlib>
 
@@ -41,8 +42,6 @@ struct HaloParams {
   int act;
   const char* res;
   int res_ld, res_off;
-  float* stats;
-  int stats_ld;
   int N, H, W;
   int TW, TH, ntx, tiles_m, tiles_n;
   int Ncols;          // valid output channels
@@ -64,17 +63,13 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void conv_halo_kernel(HaloParams
   constexpr int B_SLOTS = B_PART ? 1 : BN / RPP;
   constexpr int HS_MAX = HL_HPX / RPP;
   constexpr int BSTAGE = BN * 128;
-  constexpr int RED = (EPI == EPI_STATS) ? WGM * 2 * BN * 4 : 0;
   constexpr int PRM = (EPI == EPI_AFFINE) ? 2 * HL_MAX_AFFINE * 4 : 0;
   constexpr int NH = (BM * BN * (int)sizeof(T) > HL_HBUF) ? 2 : 1;
   constexpr int HR = BM / NH;
-  constexpr int SROWS = BM / 128;
   static_assert(TM >= 1 && TN >= 1 && HR * BN * (int)sizeof(T) <= HL_HBUF && HR % WTM == 0, "tile");
-  static_assert(WGM % SROWS == 0, "statistics rows");
-  __shared__ __attribute__((aligned(16))) char smem[2 * HL_HBUF + HL_ST * BSTAGE + RED + PRM];
+  __shared__ __attribute__((aligned(16))) char smem[2 * HL_HBUF + HL_ST * BSTAGE + PRM];
   char* const bring = smem + 2 * HL_HBUF;
-  float* red = reinterpret_cast<float*>(smem + 2 * HL_HBUF + HL_ST * BSTAGE);
-  float* prm = reinterpret_cast<float*>(smem + 2 * HL_HBUF + HL_ST * BSTAGE + RED);
+  float* prm = reinterpret_cast<float*>(smem + 2 * HL_HBUF + HL_ST * BSTAGE);
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -229,26 +224,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void conv_halo_kernel(HaloParams
           for (int b = 0; b < TN; ++b) acc[a][b][i] = 0.0f;
         }
       }
-    if constexpr (EPI == EPI_STATS) {
-#pragma unroll
-      for (int b = 0; b < TN; ++b) {
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float v = acc[a][b][i];
-            s1 += v;
-            s2 += v * v;
-          }
-        s1 += __shfl_xor(s1, 32);
-        s2 += __shfl_xor(s2, 32);
-        if (lh == 0) {
-          red[(wm * 2 + 0) * BN + wn * WTN + b * 32 + lr] = s1;
-          red[(wm * 2 + 1) * BN + wn * WTN + b * 32 + lr] = s2;
-        }
-      }
-    }
     if constexpr (EPI == EPI_AFFINE) {
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
@@ -288,21 +263,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, 1) void conv_halo_kernel(HaloParams
             }
       }
       lds_barrier();
-      if constexpr (EPI == EPI_STATS) {
-        if (h == 0 && tid < BN * SROWS) {
-          const int sr = tid / BN, c = tid - sr * BN;
-          constexpr int WPR = WGM / SROWS;
-          float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-          for (int w = 0; w < WPR; ++w) {
-            t1 += red[((sr * WPR + w) * 2 + 0) * BN + c];
-            t2 += red[((sr * WPR + w) * 2 + 1) * BN + c];
-          }
-          float* so = p.stats + (long)(tm * SROWS + sr) * 2 * p.stats_ld;
-          so[n0 + c] = t1;
-          so[p.stats_ld + n0 + c] = t2;
-        }
-      }
 #pragma unroll
       for (int j = 0; j < HR / RS; ++j) {
         const int rl = rr + RS * j;
@@ -419,8 +379,6 @@ static bool halo_geometry(const yms_conv_shape* s, int mode, HaloGeo* g) {
 
 bool conv_halo_geometry(const yms_conv_shape* s, int mode, HaloGeo* g) { return halo_geometry(s, mode, g); }
 
-int conv_halo_stats_rows(const HaloGeo& g) { return g.tiles_m * (HL_BM / 128); }
-
 // 16 waves per block (4 per SIMD) by default; YMS_HALO_WAVES=8 selects 8 (dev A/B)
 static int halo_waves() {
   static const int w = getenv("YMS_HALO_WAVES") ? atoi(getenv("YMS_HALO_WAVES")) : 16;
@@ -457,8 +415,6 @@ yms_status conv_halo_launch(const yms_conv_shape* s, int mode, const HaloGeo& g,
   p.src_ld = src_ld; p.src_off = src_off; p.dst_ld = dst_ld; p.dst_off = dst_off;
   p.scale = scale; p.shift = shift; p.act = act;
   p.res = (const char*)res; p.res_ld = res_ld; p.res_off = res_off;
-  p.stats = stats;
-  p.stats_ld = (int)rup(mode == 0 ? s->cout : s->cin, 128);
   p.N = s->n; p.H = s->h; p.W = s->w;
   p.TW = g.TW; p.TH = g.TH; p.ntx = g.ntx; p.tiles_m = g.tiles_m; p.tiles_n = g.tiles_n;
   p.Ncols = mode == 0 ? s->cout : s->cin;
@@ -473,11 +429,10 @@ yms_status conv_halo_launch(const yms_conv_shape* s, int mode, const HaloGeo& g,
   p.div_tw = make_fastdiv(g.TW);
   p.div_tw2 = make_fastdiv(g.TW + 2);
   p.div_h1 = make_fastdiv(s->h + 1);
-  if (mode == 0 && !stats && p.Ncols > HL_MAX_AFFINE) return YMS_ERR_UNSUPPORTED;
+  if (stats || (mode == 0 && p.Ncols > HL_MAX_AFFINE)) return YMS_ERR_UNSUPPORTED;
 #define YMS_HALO_CASE(T)                                                                   \
   if (mode == 0) {                                                                         \
-    if (stats) launch_halo<T, MODE_FWD, EPI_STATS>(p, g.bn, st);                           \
-    else launch_halo<T, MODE_FWD, EPI_AFFINE>(p, g.bn, st);                                \
+    launch_halo<T, MODE_FWD, EPI_AFFINE>(p, g.bn, st);                                     \
   } else {                                                                                 \
     if (accumulate) launch_halo<T, MODE_DGRAD, EPI_ACCUM>(p, g.bn, st);                    \
     else launch_halo<T, MODE_DGRAD, EPI_STORE>(p, g.bn, st);                               \

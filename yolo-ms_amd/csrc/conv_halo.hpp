@@ -12,7 +12,6 @@ struct HaloGeo {
 // mode 0 = forward, 1 = stride-1 input gradient.  False when the shape / dtype is not handled
 // (the im2col NT kernel runs instead) or YMS_HALO=0.
 bool conv_halo_geometry(const yms_conv_shape* s, int mode, HaloGeo* g);
-int conv_halo_stats_rows(const HaloGeo& g);
 yms_status conv_halo_launch(const yms_conv_shape* s, int mode, const HaloGeo& g, const void* src, int src_ld,
                             int src_off, const void* wpacked, void* dst, int dst_ld, int dst_off, const float* scale,
                             const float* shift, int act, const void* res, int res_ld, int res_off, float* stats,

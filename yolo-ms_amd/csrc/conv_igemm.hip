@@ -332,13 +332,11 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
   const int ch = tid % CH, rr = tid / CH;
   const int col0 = n0 + ch * 8;
   const int nv = p.Ncols - col0;          // valid channels in this chunk (may be <= 0)
-  float sc[8], sh[8], s1[8], s2[8];
+  float sc[8], sh[8];
 #pragma unroll
   for (int i = 0; i < 8; ++i) {
     sc[i] = 1.0f;
     sh[i] = 0.0f;
-    s1[i] = 0.0f;
-    s2[i] = 0.0f;
     if (EPI == EPI_AFFINE && i < nv) {
       if (p.scale) sc[i] = p.scale[col0 + i];
       if (p.shift) sh[i] = p.shift[col0 + i];
@@ -353,13 +351,6 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
     const float4 u1 = *reinterpret_cast<const float4*>(st + rl * EPI_P + ch * 8 + 4);
     v[0] = u0.x; v[1] = u0.y; v[2] = u0.z; v[3] = u0.w;
     v[4] = u1.x; v[5] = u1.y; v[6] = u1.z; v[7] = u1.w;
-    if (EPI == EPI_STATS) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        s1[i] += v[i];
-        s2[i] += v[i] * v[i];
-      }
-    }
     if (row >= M || nv <= 0) continue;
     if (MODE == MODE_DGRAD2) {
       const uint32_t n = fdiv((uint32_t)row, dv_hw);
@@ -391,19 +382,17 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
     store8(dst, nv, v);
   }
   if (EPI == EPI_STATS) {
-    __syncthreads();                      // staging tile no longer read
-    float* red = reinterpret_cast<float*>(smem);  // [2][RS][BN]
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      red[rr * BN + ch * 8 + i] = s1[i];
-      red[RS * BN + rr * BN + ch * 8 + i] = s2[i];
-    }
-    __syncthreads();
+    // one statistics row per 128-row tile (BM == 128): sum and centred M2 of each column over
+    // the valid rows, two passes down the fp32 staging tile (read-only since the barrier above)
+    static_assert(EPI != EPI_STATS || BM == 128, "statistics rows are 128 output rows");
     if (tid < BN) {
+      const int nrow = min(BM, M - m0);
       float t1 = 0.f, t2 = 0.f;
-      for (int w = 0; w < RS; ++w) {
-        t1 += red[w * BN + tid];
-        t2 += red[RS * BN + w * BN + tid];
+      for (int r = 0; r < nrow; ++r) t1 += st[r * EPI_P + tid];
+      const float mu = t1 / (float)nrow;
+      for (int r = 0; r < nrow; ++r) {
+        const float d = st[r * EPI_P + tid] - mu;
+        t2 += d * d;
       }
       float* so = p.stats + (long)tile_m * 2 * p.stats_ld;
       so[n0 + tid] = t1;
@@ -643,19 +632,11 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
     T* stg = reinterpret_cast<T*>(smem + stage * STAGE);
     // per-column parameters / statistics from the fp32 accumulators
     if constexpr (EPI == EPI_STATS) {
+      const int nw = min(WTM, max(0, M - (m0 + wm * WTM)));   // valid rows of this wave
 #pragma unroll
       for (int b = 0; b < TN; ++b) {
-        float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-        for (int a = 0; a < TM; ++a)
-#pragma unroll
-          for (int i = 0; i < 16; ++i) {
-            const float v = acc[a][b][i];
-            s1 += v;
-            s2 += v * v;
-          }
-        s1 += __shfl_xor(s1, 32);
-        s2 += __shfl_xor(s2, 32);
+        float s1, s2;
+        wave_col_moments<TM>(acc, b, nw, lh, s1, s2);
         if (lh == 0) {
           red[(wm * 2 + 0) * BN + wn * WTN + b * 32 + lr] = s1;
           red[(wm * 2 + 1) * BN + wn * WTN + b * 32 + lr] = s2;
@@ -706,13 +687,10 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
         if (h == 0 && tid < BN * SROWS) {
           const int sr = tid / BN, c = tid - sr * BN;
           constexpr int WPR = WGM / SROWS;    // wave rows per statistics row
-          float t1 = 0.f, t2 = 0.f;
-#pragma unroll
-          for (int w = 0; w < WPR; ++w) {
-            t1 += red[((sr * WPR + w) * 2 + 0) * BN + c];
-            t2 += red[((sr * WPR + w) * 2 + 1) * BN + c];
-          }
           const int srow = tile_m * SROWS + sr;
+          float t1, t2;
+          merge_moments<WPR, WTM>(red + (sr * WPR * 2 + 0) * BN + c, red + (sr * WPR * 2 + 1) * BN + c, 2 * BN,
+                                  M - srow * 128, t1, t2);
           if (srow * 128 < M) {
             float* so = p.stats + (long)srow * 2 * p.stats_ld;
             so[n0 + c] = t1;
@@ -1469,8 +1447,6 @@ yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* p
 
 int yms_conv_stats_rows(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
-  HaloGeo hg;
-  if (conv_halo_geometry(s, 0, &hg)) return conv_halo_stats_rows(hg);
   TileChoice tc = choose_tile(s->cout);
   return rows_for(s->n * s->ho * s->wo, tc.cfg);
 }
@@ -1487,7 +1463,7 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   if (!view_ok(x_ld, x_off, s->cin) || !view_ok(y_ld, y_off, s->cout)) return YMS_ERR_INVALID;
   if (res && !view_ok(res_ld, res_off, s->cout)) return YMS_ERR_INVALID;
   const int es = elem_size(s->dtype);
-  {
+  if (!stats) {   // statistics rows come from the NT kernels only
     HaloGeo hg;
     if (conv_halo_geometry(s, 0, &hg))
       return conv_halo_launch(s, 0, hg, x, x_ld, x_off, wpacked, y, y_ld, y_off, scale, shift, act, res, res_ld,

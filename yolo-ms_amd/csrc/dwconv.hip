@@ -115,9 +115,6 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
   }
   const int c = c0 + 8 * g, nv = min(8, p.C - c);
   const int y = y0 + ty;
-  float s1[8], s2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { s1[k] = 0.f; s2[k] = 0.f; }
   float sc[8], sh[8];
   if (MODE == DW_FWD_AFFINE) {
 #pragma unroll
@@ -140,10 +137,6 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
           v = v * sc[k] + sh[k];
           if (p.act == YMS_ACT_SILU) v = silu_f(v);
         }
-        if (MODE == DW_FWD_STATS) {
-          s1[k] += v;
-          s2[k] += v * v;
-        }
         o[k] = v;
       }
       T* d = dst + (((long)n * p.H + y) * p.W + x) * p.dst_ld + p.dst_off + c;
@@ -157,20 +150,42 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
     }
   }
   if (MODE == DW_FWD_STATS) {
-    // one statistics row per spatial tile: wave butterfly over the 64 pixel lanes (fixed order)
+    // one statistics row per spatial tile (conv_common.hpp contract, row counts from
+    // yms_dwconv_stats_counts): sum and centred M2 over the tile's valid pixels, two passes over
+    // the fp32 accumulators, wave butterflies in a fixed order
+    const int vy = min(DW_TY, p.H - y0), vx = min(DW_TX, p.W - x0);
+    const float inv_n = 1.0f / (float)(vy * vx);
+    float s1[8], m2[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
+      float s = 0.f;
+      if (y < p.H) {
 #pragma unroll
-      for (int m = 1; m < 64; m <<= 1) {
-        s1[k] += __shfl_xor(s1[k], m);
-        s2[k] += __shfl_xor(s2[k], m);
+        for (int i = 0; i < DW_RX; ++i)
+          if (x0 + 4 * qx + i < p.W) s += acc[i][k];
       }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
+      const float mu = s * inv_n;
+      float q = 0.f;
+      if (y < p.H) {
+#pragma unroll
+        for (int i = 0; i < DW_RX; ++i)
+          if (x0 + 4 * qx + i < p.W) {
+            const float d = acc[i][k] - mu;
+            q += d * d;
+          }
+      }
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) q += __shfl_xor(q, m);
+      s1[k] = s;
+      m2[k] = q;
     }
     if (lane < 8 && c + lane < p.C) {
       float a = 0.f, b = 0.f;
 #pragma unroll
       for (int k = 0; k < 8; ++k)
-        if (k == lane) { a = s1[k]; b = s2[k]; }
+        if (k == lane) { a = s1[k]; b = m2[k]; }
       float* so = p.stats + (long)tile * 2 * p.stats_ld;
       so[c + lane] = a;
       so[p.stats_ld + c + lane] = b;
@@ -335,6 +350,18 @@ int yms_dwconv_stats_rows(const yms_dw_shape* s) {
   if (!dw_shape_ok(s)) return 0;
   int tx, ty;
   return dw_tiles(s, tx, ty);
+}
+
+yms_status yms_dwconv_stats_counts(const yms_dw_shape* s, float* counts) {
+  if (!dw_shape_ok(s) || !counts) return YMS_ERR_INVALID;
+  int tx, ty;
+  const int rows = dw_tiles(s, tx, ty);
+  for (int r = 0; r < rows; ++r) {
+    const int rem = r % (tx * ty);
+    const int y0 = (rem / tx) * DW_TY, x0 = (rem % tx) * DW_TX;
+    counts[r] = (float)(std::min(DW_TY, s->h - y0) * std::min(DW_TX, s->w - x0));
+  }
+  return YMS_OK;
 }
 
 yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,

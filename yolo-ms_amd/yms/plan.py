@@ -224,6 +224,10 @@ class ConvOp:
             self.cnt = plan.counter()
             plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
 
+    def row_counts(self):
+        """Pixels per BN statistics row: None = the convolutions' 128-pixel rows."""
+        return None
+
     def pack_specs(self):
         """(shape, fp32 weight, arena byte offset of the packed copy, for_dgrad) per training pack."""
         w = self.mod.conv.weight.data_ptr()
@@ -256,7 +260,8 @@ class ConvOp:
         L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
                None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
         bn = m.bn
-        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
+        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, self.row_counts(),
+               bn.weight.data_ptr(),
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
@@ -373,6 +378,146 @@ class BiasConvOp:
         return [self.pbias, self.pw]
 
 
+class DWConvOp(ConvOp):
+    """Depthwise Conv block (YOLO-MS IB_k mid conv, yolov8/model/yolo_ms.py): Conv2d(groups=C,
+    bias=False, k x k, stride 1, pad k//2) -> BatchNorm2d -> SiLU, on the dwconv kernels.  BN
+    forward/backward are the ConvOp path; weights are read unpacked (fp32 [C][k][k])."""
+
+    def __init__(self, b, mod, x, y, act):
+        conv = mod.conv
+        k = conv.kernel_size[0]
+        c = conv.out_channels
+        if not (conv.groups == c == conv.in_channels and conv.kernel_size[0] == conv.kernel_size[1]
+                and k in (3, 5, 7, 9) and conv.stride == (1, 1) and conv.padding == (k // 2, k // 2)
+                and conv.dilation == (1, 1)):
+            raise RuntimeError("yms: grouped convolutions are supported as depthwise k x k (k = 3/5/7/9), "
+                               "stride 1, pad k//2")
+        self.mod, self.x, self.y, self.res, self.act = mod, x, y, None, act
+        self.dshape = L.DwShape(b.n, x.h, x.w, c, k, b.dt)
+        self.sp = ctypes.pointer(self.dshape)
+        self.c = c
+        self.npix = b.n * y.h * y.w
+        self.pw = b.param(conv, "weight")
+        self.pg = b.param(mod.bn, "weight")
+        self.pb = b.param(mod.bn, "bias")
+        self.flops = 0          # not an MFMA contraction: excluded from the conv roofline
+        self.dw_flops = 2 * self.npix * c * k * k
+
+    def layout(self, plan, La, Le):
+        es, c = plan.es, self.c
+        self.e_sc = Le.alloc(4 * c)
+        self.e_sh = Le.alloc(4 * c)
+        if plan.training:
+            self.zld = r8(c)
+            self.z = La.alloc(self.npix * self.zld * es)
+            self.sc = La.alloc(4 * c)
+            self.sh = La.alloc(4 * c)
+            self.mi = La.alloc(8 * c)
+            self.stats_rows = L.lib().yms_dwconv_stats_rows(self.sp)
+            self.stats_ld = r8(c)
+            plan.need_scratch("stats", 4 * 2 * self.stats_rows * self.stats_ld)
+            plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
+            plan.need_scratch("coef", 8 * c)
+            plan.need_scratch("wgrad", L.lib().yms_dwconv_wgrad_ws_bytes(self.sp))
+            self.cnt = plan.counter()
+            counts = torch.empty(self.stats_rows, dtype=torch.float32)
+            L.call("yms_dwconv_stats_counts", self.sp, counts.data_ptr())
+            self.counts_host, self.counts_dev = counts, None
+
+    def row_counts(self):
+        """Pixels per statistics row (one 8x32 tile each): a static table, uploaded once."""
+        if self.counts_dev is None:
+            self.counts_dev = self.counts_host.to(torch.device("cuda", torch.cuda.current_device()))
+        return self.counts_dev.data_ptr()
+
+    def pack_specs(self):
+        return []
+
+    def prepare_eval(self, rt):
+        bn = self.mod.bn
+        L.call("yms_bn_fold", self.c, bn.weight.data_ptr(), bn.bias.data_ptr(), bn.running_mean.data_ptr(),
+               bn.running_var.data_ptr(), ctypes.c_float(bn.eps), rt.eval_base + self.e_sc,
+               rt.eval_base + self.e_sh, rt.st)
+
+    def fwd(self, rt):
+        x, y = self.x, self.y
+        w = self.mod.conv.weight.data_ptr()
+        if not rt.training:
+            eb = rt.eval_base
+            L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, rt.a(y), y.buf.ld, y.off, eb + self.e_sc,
+                   eb + self.e_sh, self.act, None, 0, rt.st)
+            return
+        base = rt.base
+        stats = base + rt.plan.scratch["stats"]
+        L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, base + self.z, self.zld, 0, None, None,
+               L.ACT_NONE, stats, self.stats_ld, rt.st)
+        bn = self.mod.bn
+        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, self.row_counts(),
+               bn.weight.data_ptr(),
+               bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+               ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
+               ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
+        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+               base + self.sh, self.act, None, 0, 0, rt.a(y), y.buf.ld, y.off, rt.st)
+
+    def bwd(self, rt):
+        x, y = self.x, self.y
+        base, dt, c = rt.base, rt.plan.dt, self.c
+        z = base + self.z
+        ws = rt.gbase + rt.plan.gscratch["bwd"]
+        coef = rt.gbase + rt.plan.gscratch["coef"]
+        L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, rt.g(y), y.buf.ld, y.off, base + self.sc,
+               base + self.sh, base + self.mi, self.act, ws, rt.st)
+        L.call("yms_bn_act_bwd_finalize", c, ws, L.lib().yms_bn_bwd_rows(self.npix, c), self.npix,
+               rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, rt.g(y), y.buf.ld, y.off, base + self.sc,
+               base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, None, 0, 0, 0, rt.st)
+        w = self.mod.conv.weight.data_ptr()
+        if x.buf.needs_grad:
+            L.call("yms_dwconv_dgrad", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
+        dw = rt.pgrad(self.pw)
+        if dw is not None:
+            wsz = L.lib().yms_dwconv_wgrad_ws_bytes(self.sp)
+            L.call("yms_dwconv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
+                   rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
+
+
+class AddOp:
+    """y = a + b (b None: y = a) over channel views: the MS-Block branch sums X_i + Y_{i-1} and
+    the Y_1 = X_1 placement.  Backward routes dy into both addends (store or accumulate)."""
+
+    def __init__(self, b, a, bb, y):
+        self.a, self.b, self.y = a, bb, y
+        self.npix = b.n * y.h * y.w
+        self.c = y.c
+        self.flops = 0
+
+    def layout(self, plan, La, Le):
+        pass
+
+    def fwd(self, rt):
+        a, b, y = self.a, self.b, self.y
+        bp = rt.a(b) if b is not None else None
+        bl, bo = (b.buf.ld, b.off) if b is not None else (0, 0)
+        L.call("yms_add_views", rt.plan.dt, self.npix, self.c, rt.a(a), a.buf.ld, a.off, bp, bl, bo, rt.a(y),
+               y.buf.ld, y.off, 0, rt.st)
+
+    def plan_grads(self, T):
+        T.read(self.y)
+        self.acc = [T.write(v) if (v is not None and v.buf.needs_grad) else None for v in (self.a, self.b)]
+
+    def bwd(self, rt):
+        y = self.y
+        for v, acc in zip((self.a, self.b), self.acc):
+            if v is None or acc is None:
+                continue
+            L.call("yms_add_views", rt.plan.dt, self.npix, self.c, rt.g(y), y.buf.ld, y.off, None, 0, 0, rt.g(v),
+                   v.buf.ld, v.off, acc, rt.st)
+
+    def grad_params(self):
+        return []
+
+
 class UpsampleOp:
     """nearest x2, components.py:153-160."""
 
@@ -463,7 +608,21 @@ class Builder:
         assert out.c == conv.out_channels and out.h == ho and out.w == wo, "yms: output view mismatch"
         if act is None:
             act = L.ACT_SILU if isinstance(mod.activation, torch.nn.SiLU) else L.ACT_NONE
-        self.ops.append(ConvOp(self, mod, x, out, res, act))
+        if conv.groups != 1:
+            if res is not None:
+                raise RuntimeError("yms: residual epilogue is not supported on depthwise convolutions")
+            self.ops.append(DWConvOp(self, mod, x, out, act))
+        else:
+            self.ops.append(ConvOp(self, mod, x, out, res, act))
+        return out
+
+    def add(self, a, b, out=None):
+        """y = a + b (b may be None: a placement copy) -> view."""
+        if b is not None and (a.h, a.w, a.c) != (b.h, b.w, b.c):
+            raise RuntimeError("yms: add of mismatched views")
+        if out is None:
+            out = self.new(a.h, a.w, a.c)
+        self.ops.append(AddOp(self, a, b, out))
         return out
 
     def conv2d_bias(self, conv, x, out=None):

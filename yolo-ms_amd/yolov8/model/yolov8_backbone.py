@@ -24,6 +24,11 @@ class Backbone(_YmsModule):
         self.c2f_8 = C2f(c5, c5, num_bottlenecks=int(3 * d), shortcut=True)
         self.sppf = SPPF(c5, c5, kernel_size=5)
 
+    def out_channels(self):
+        """(P3, P4, P5) channels."""
+        return (self.c2f_4.conv2.conv.out_channels, self.c2f_6.conv2.conv.out_channels,
+                self.sppf.conv2.conv.out_channels)
+
     def emit(self, b, x, outs=(None, None, None)):
         x = self.conv0.emit(b, x)
         x = self.conv1.emit(b, x)

@@ -22,9 +22,17 @@ class Neck(_YmsModule):
         self.conv1 = Conv(int(256 * w), int(256 * w), kernel_size=3, stride=2, padding=1)
         self.conv2 = Conv(int(512 * w), int(512 * w), kernel_size=3, stride=2, padding=1)
 
+    def _stage(self, i):
+        """Fusion block i (1..4): C2f here, MSBlock in the YOLO-MS neck (yolo_ms.MSNeck)."""
+        return getattr(self, f"c2f_{i}")
+
+    def _stage_out(self, i):
+        m = self._stage(i)
+        return m.conv2.conv.out_channels if hasattr(m, "conv2") else m.out_channels
+
     def alloc_cats(self, b, h3, w3, c3, h4, w4, c4, h5, w5, c5):
         """The four concat buffers; returns them and the slots P3/P4/P5 must occupy."""
-        cr2 = self.c2f_1.conv2.conv.out_channels          # res_2 channels
+        cr2 = self._stage_out(1)                           # res_2 channels
         cc1 = self.conv1.conv.out_channels
         cc2 = self.conv2.conv.out_channels
         cat1 = b.new(h4, w4, c5 + c4, name="neck_cat1")     # [up(P5), P4]
@@ -39,17 +47,17 @@ class Neck(_YmsModule):
             raise RuntimeError("yms: Neck.emit needs its concat buffers (use alloc_cats)")
         cat1, cat2, cat3, cat4 = cats
         c5, c4, c3 = p5.c, p4.c, p3.c
-        cr2 = self.c2f_1.conv2.conv.out_channels
+        cr2 = self._stage_out(1)
         cc1 = self.conv1.conv.out_channels
         cc2 = self.conv2.conv.out_channels
         self.up.emit(b, p5, out=cat1.slot(0, c5))
-        res_2 = self.c2f_1.emit(b, cat1, out=cat3.slot(cc1, cr2))
+        res_2 = self._stage(1).emit(b, cat1, out=cat3.slot(cc1, cr2))
         self.up.emit(b, res_2, out=cat2.slot(0, cr2))
-        out1 = self.c2f_2.emit(b, cat2, out=outs[0])
+        out1 = self._stage(2).emit(b, cat2, out=outs[0])
         self.conv1.emit(b, out1, out=cat3.slot(0, cc1))
-        out2 = self.c2f_3.emit(b, cat3, out=outs[1])
+        out2 = self._stage(3).emit(b, cat3, out=outs[1])
         self.conv2.emit(b, out2, out=cat4.slot(0, cc2))
-        out3 = self.c2f_4.emit(b, cat4, out=outs[2])
+        out3 = self._stage(4).emit(b, cat4, out=outs[2])
         return out1, out2, out3
 
     def _yms_plan(self, b, inputs):

@@ -13,12 +13,20 @@ from torch import nn
 from yolov8.model.yolov8_backbone import Backbone
 from yolov8.model.yolov8_neck import Neck
 from yolov8.model.yolov8_head import Head
+from yolov8.model.yolo_ms import MSBackbone, MSNeck, is_ms_version, ms_params
 from yms import runner as _runner
 
 
 class YOLOv8(nn.Module):
     def __init__(self, version: str, num_classes: int, dfl_ch: int = 16) -> None:
         super().__init__()
+        if is_ms_version(version):
+            # YOLO-MS family ('ms-xs', 'ms-s', 'ms-l'): MS-Block / HKS backbone and neck, the
+            # reference head (yolov8/model/yolo_ms.py; not in the reference's code)
+            self.backbone = MSBackbone(version)
+            self.neck = MSNeck(version)
+            self.head = Head(version=ms_params(version)[4], num_classes=num_classes, ch=dfl_ch)
+            return
         self.backbone = Backbone(version)
         self.neck = Neck(version)
         self.head = Head(version=version, num_classes=num_classes, ch=dfl_ch)
@@ -30,9 +38,7 @@ class YOLOv8(nn.Module):
             raise RuntimeError(f"yms: input size must be a multiple of 32, got {H}x{W}")
         xin = b.new(H, W, x.shape[1], name="input")
         bb, nk = self.backbone, self.neck
-        c3 = bb.c2f_4.conv2.conv.out_channels
-        c4 = bb.c2f_6.conv2.conv.out_channels
-        c5 = bb.sppf.conv2.conv.out_channels
+        c3, c4, c5 = bb.out_channels()
         cats, slots = nk.alloc_cats(b, H // 8, W // 8, c3, H // 16, W // 16, c4, H // 32, W // 32, c5)
         p3, p4, p5 = bb.emit(b, xin, outs=slots)
         f = nk.emit(b, p3, p4, p5, cats=cats)
