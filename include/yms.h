@@ -80,14 +80,15 @@ yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* pack
 yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev, void* dst_base, void* stream);
 
 /* ---- convolution (implicit GEMM on MFMA) --------------------------------------------- */
-/* Number of fp32 rows of BN partial statistics written by yms_conv_fwd(stats != NULL): one per
- * 128 output pixels (ceil(n*ho*wo / 128)); the stats workspace is [rows][2][stats_ld] floats,
- * stats_ld = yms_conv_stats_ld(). */
+/* Rows of BN partial statistics written by yms_conv_fwd(stats != NULL): fp32 -- one per 128
+ * output pixels; bf16/f16 -- one per persistent block (and 128-row half of its tiles).  The stats
+ * workspace is [rows][2][stats_ld] floats followed by [rows] float pixel counts (so
+ * rows * (2*stats_ld + 1) floats), stats_ld = yms_conv_stats_ld(). */
 int yms_conv_stats_rows(const yms_conv_shape* s);
 int yms_conv_stats_ld(const yms_conv_shape* s);
 /* Forward.  stats == NULL: y = act(conv(x)*scale[c] + shift[c]) (+ res) (scale/shift may
- * be NULL = identity).  stats != NULL (training): y = conv(x) (pre-BN z) and per-128-pixel
- * rows (sum z, sum (z - row mean)^2) into stats. */
+ * be NULL = identity).  stats != NULL (training): y = conv(x) (pre-BN z) and statistics rows
+ * (sum z, sum (z - row mean)^2, pixel count) into stats. */
 yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
                         const void* wpacked, void* y, int y_ld, int y_off,
                         const float* scale, const float* shift, int act,
@@ -108,11 +109,10 @@ yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float
                        const float* rvar, float eps, float* scale, float* shift, void* stream);
 /* Train: merge the statistics rows of `count` pixels -> mean/invstd, scale/shift, and update the
  * running buffers (unbiased var, momentum) exactly like nn.BatchNorm2d.  mean_invstd: [2][c].
- * Row r = (sum z, sum (z - mean_r)^2) over n_r pixels: n_r = row_counts[r] when row_counts is
- * given (yms_dwconv_stats_counts), else min(128, count - 128 r) (the convolutions' rows, which
- * requires 128 (rows - 1) < count <= 128 rows).  Rows are merged with Chan's update in fp64.
+ * Row r = (sum z, sum (z - mean_r)^2) over n_r pixels, n_r = ((float*)stats)[rows*2*stats_ld + r]
+ * (the producers' count table; empty rows allowed); rows are merged with Chan's update in fp64.
  * The stats table is consumed: long tables are pre-reduced in place. */
-yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count, const float* row_counts,
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream);
@@ -188,11 +188,9 @@ typedef struct {
 } yms_dw_shape;
 /* rows of BN partial statistics written by yms_dwconv_fwd(stats != NULL): one per 8x32 tile */
 int yms_dwconv_stats_rows(const yms_dw_shape* s);
-/* host: pixels of each statistics row (the tile's in-image extent) -> counts[rows], for
- * yms_bn_finalize's row_counts */
-yms_status yms_dwconv_stats_counts(const yms_dw_shape* s, float* counts);
 /* stats == NULL: y = act(conv*scale + shift) (scale/shift NULL = identity); else y = conv (pre-BN
- * z) and per-tile (sum z, sum (z - tile mean)^2) rows [rows][2][stats_ld]. */
+ * z) and per-tile (sum z, sum (z - tile mean)^2) rows [rows][2][stats_ld] followed by [rows] pixel
+ * counts. */
 yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
                           int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
                           int stats_ld, void* stream);

@@ -46,34 +46,49 @@ def conv_fwd(xb, w, sh, dtype, scale=None, shift=None, act=0, res=None, stats=Fa
     wp = pack(w, sh, dtype, 0)
     yld = yld or r8(yoff + sh.cout)
     y = torch.zeros((sh.n, sh.ho, sh.wo, yld), dtype=dtype, device="cuda")
-    st = None
+    st, buf = None, None
     if stats:
         rows, ld = L.lib().yms_conv_stats_rows(sp), L.lib().yms_conv_stats_ld(sp)
-        st = torch.zeros((rows, 2, ld), dtype=torch.float32, device="cuda")
+        buf = stats_buffer(rows, ld)
+        st = split_stats(buf, rows, ld)
     L.call("yms_conv_fwd", sp, xb.data_ptr(), xb.shape[-1], xoff, wp.data_ptr(), y.data_ptr(), yld, yoff,
            L.ptr(scale), L.ptr(shift), act, L.ptr(res), res.shape[-1] if res is not None else 0, 0,
-           L.ptr(st), L.stream_ptr())
+           L.ptr(buf), L.stream_ptr())
     return y, st
 
 
-def merge_moments(st, c, npix, counts=None):
-    """BN statistics rows [rows][2][ld] (sum z, sum (z - row mean)^2 over n_r pixels; n_r = counts or
-    the 128-pixel rule) -> (sum z, M2 about the global mean) per channel, fp64 on the host."""
-    st = st.double().cpu()
-    rows = st.shape[0]
-    if counts is None:
-        counts = torch.clamp(npix - 128 * torch.arange(rows, dtype=torch.float64), max=128.0)
-    n = torch.as_tensor(counts, dtype=torch.float64).cpu().view(-1, 1)
-    s1, m2 = st[:, 0, :c], st[:, 1, :c]
+def stats_buffer(rows, ld):
+    """BN statistics workspace: [rows][2][ld] moments + [rows] pixel counts, NaN-filled so a row the
+    producer did not write shows up."""
+    return torch.full((rows * (2 * ld + 1),), float("nan"), dtype=torch.float32, device="cuda")
+
+
+def split_stats(buf, rows, ld):
+    """-> (moment rows [rows, 2, ld], counts [rows]) views of a statistics workspace."""
+    return buf[:rows * 2 * ld].view(rows, 2, ld), buf[rows * 2 * ld:]
+
+
+def merge_moments(st, c, npix):
+    """BN statistics (moment rows [rows][2][ld] = (sum z, sum (z - row mean)^2) over n_r pixels,
+    counts [rows] = n_r) -> (sum z, M2 about the global mean) per channel, fp64 on the host.  Every
+    row must have been written, and the counts must add up to npix."""
+    rows_, counts = st
+    rows_, n = rows_.double().cpu(), counts.double().cpu().view(-1, 1)
+    assert torch.isfinite(rows_[:, :, :c]).all() and torch.isfinite(n).all()
+    assert n.sum().item() == npix, (n.sum().item(), npix)
+    s1, m2 = rows_[:, 0, :c], rows_[:, 1, :c]
     mean = s1.sum(0) / npix
+    keep = (n > 0).view(-1)
+    s1, m2, n = s1[keep], m2[keep], n[keep]
     return s1.sum(0), (m2 + n * (s1 / n - mean) ** 2).sum(0)
 
 
-def check_moments(st, z, tol, counts=None):
-    """Statistics rows of the pre-BN tensor z (NCHW fp32) against its exact sum and centred M2."""
+def check_moments(st, z, tol):
+    """Statistics (moment rows, counts) of the pre-BN tensor z (NCHW fp32) against its exact sum
+    and centred M2."""
     c = z.shape[1]
     npix = z.numel() // c
-    s1, m2 = merge_moments(st, c, npix, counts)
+    s1, m2 = merge_moments(st, c, npix)
     zd = z.double()
     ref1 = zd.sum((0, 2, 3))
     ref2 = ((zd - zd.mean((0, 2, 3), keepdim=True)) ** 2).sum((0, 2, 3))

@@ -97,54 +97,67 @@ def test_bias_bwd_fused():
         assert int(cnt[0]) == 0
 
 
-def _finalize(st, c, npix, counts=None):
+def _finalize(buf, rows, ld, c, npix):
     gam = torch.rand(c, generator=torch.Generator().manual_seed(c)).cuda() + 0.5
     bet = torch.randn(c, generator=torch.Generator().manual_seed(c + 1)).cuda()
     rm, rv = torch.zeros(c, device="cuda"), torch.ones(c, device="cuda")
     mi = torch.empty(2 * c, device="cuda")
     sc, sh = torch.empty(c, device="cuda"), torch.empty(c, device="cuda")
-    L.call("yms_bn_finalize", c, st.data_ptr(), st.shape[0], st.shape[2], npix, L.ptr(counts), gam.data_ptr(),
-           bet.data_ptr(), rm.data_ptr(), rv.data_ptr(), ctypes.c_float(0.03), ctypes.c_float(1e-3), mi.data_ptr(),
-           sc.data_ptr(), sh.data_ptr(), L.stream_ptr())
+    L.call("yms_bn_finalize", c, buf.data_ptr(), rows, ld, npix, gam.data_ptr(), bet.data_ptr(), rm.data_ptr(),
+           rv.data_ptr(), ctypes.c_float(0.03), ctypes.c_float(1e-3), mi.data_ptr(), sc.data_ptr(), sh.data_ptr(),
+           L.stream_ptr())
     torch.cuda.synchronize()
     return mi[:c].double().cpu(), mi[c:].double().cpu(), rv.double().cpu()
 
 
-@pytest.mark.parametrize("b,h,w,offset", [(2, 3, 2, 300.0), (4, 40, 40, 1000.0), (9, 80, 80, 50.0)])
-def test_bn_stats_large_mean_conv_and_dw(b, h, w, offset):
+@pytest.mark.parametrize("b,h,w,offset,dt", [(2, 3, 2, 300.0, "f32"), (4, 40, 40, 1000.0, "f32"),
+                                             (9, 80, 80, 50.0, "f32"), (16, 80, 80, 300.0, "bf16"),
+                                             (3, 17, 23, 1000.0, "bf16")])
+def test_bn_stats_large_mean_conv_and_dw(b, h, w, offset, dt):
     """Training BN statistics where |mean| / std ~ 4e2-8e3 (sum z^2 - n mean^2 in fp32 would lose
-    every digit): conv (128-pixel rows; > 256 rows exercises the in-place pre-reduction) and
-    depthwise (8x32 tile rows with a row-count table) against fp64 moments of the kernels' own
-    fp32 z, through yms_bn_finalize."""
-    from hiputil import conv_fwd, nchw, nhwc, shape, r8
+    every digit): conv (fp32: 128-pixel rows, > 1024 rows exercises the in-place pre-reduction;
+    bf16: per-block slot rows) and depthwise (8x32 tile rows) against fp64 moments of the
+    kernels' own z, through yms_bn_finalize and the producers' count tables."""
+    from hiputil import DT, conv_fwd, nchw, nhwc, r8, ref_conv, shape, stats_buffer
+    dtype = DT[dt]
     c = 64
     g = torch.Generator().manual_seed(b * h)
     x = offset + torch.randn(b, c, h, w, generator=g)
     wt = (torch.rand(c, c, 1, 1, generator=g) + 0.5) / c
-    sp = shape(b, h, w, c, c, 1, 1, torch.float32)
-    y, st = conv_fwd(nhwc(x, torch.float32), wt, sp, torch.float32, stats=True)
-    z = nchw(y, c).double().cpu()
-    mean, istd, rv = _finalize(st, c, b * h * w)
-    var = z.var((0, 2, 3), unbiased=False)
-    assert ((mean - z.mean((0, 2, 3))).abs() / z.mean((0, 2, 3)).abs()).max().item() < 1e-6
-    assert ((istd - 1 / (var + 1e-3).sqrt()).abs() * (var + 1e-3).sqrt()).max().item() < 1e-4
+    sp = shape(b, h, w, c, c, 1, 1, dtype)
+    y, (st, cnt) = conv_fwd(nhwc(x, dtype), wt, sp, dtype, stats=True)
     n = b * h * w
+    assert cnt.sum().item() == n
+    # statistics come from the fp32 accumulators: compare with the fp32 conv of the same operands
+    z = ref_conv(x, wt, 1, dtype).double() if dt == "bf16" else nchw(y, c).double().cpu()
+    rows, ld = st.shape[0], st.shape[2]
+    mean, istd, rv = _finalize(_flat(st, cnt), rows, ld, c, n)
+    var = z.var((0, 2, 3), unbiased=False)
+    tol = 1e-6 if dt == "f32" else 2e-6
+    assert ((mean - z.mean((0, 2, 3))).abs() / z.mean((0, 2, 3)).abs()).max().item() < tol
+    assert ((istd - 1 / (var + 1e-3).sqrt()).abs() * (var + 1e-3).sqrt()).max().item() < 1e-4
     assert ((rv - (0.97 + 0.03 * var * n / (n - 1))).abs() / rv).max().item() < 1e-5
     # depthwise 3x3 on the same large-offset input
-    ds = L.DwShape(b, h, w, c, 3, L.F32)
+    ds = L.DwShape(b, h, w, c, 3, L.dtype_code(dtype))
     dsp = ctypes.pointer(ds)
     wd = (torch.rand(c, 1, 3, 3, generator=g) + 0.5).cuda() / 9
-    rows = L.lib().yms_dwconv_stats_rows(dsp)
-    sd = torch.full((rows, 2, r8(c)), float("nan"), device="cuda")
-    counts = torch.empty(rows)
-    L.call("yms_dwconv_stats_counts", dsp, counts.data_ptr())
-    assert counts.sum().item() == n
-    xb = nhwc(x, torch.float32)
-    yd = torch.zeros((b, h, w, r8(c)), device="cuda")
+    drows = L.lib().yms_dwconv_stats_rows(dsp)
+    dbuf = stats_buffer(drows, r8(c))
+    xb = nhwc(x, dtype)
+    yd = torch.zeros((b, h, w, r8(c)), dtype=dtype, device="cuda")
     L.call("yms_dwconv_fwd", dsp, xb.data_ptr(), xb.shape[-1], 0, wd.data_ptr(), yd.data_ptr(), yd.shape[-1], 0,
-           None, None, 0, sd.data_ptr(), r8(c), L.stream_ptr())
-    zd = nchw(yd, c).double().cpu()
-    mean, istd, _ = _finalize(sd, c, n, counts.cuda())
+           None, None, 0, dbuf.data_ptr(), r8(c), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert dbuf[drows * 2 * r8(c):].sum().item() == n
+    zd = torch.nn.functional.conv2d(x.to(dtype).double(), wd.double().cpu(), None, 1, 1, 1, c)
+    mean, istd, _ = _finalize(dbuf, drows, r8(c), c, n)
     var = zd.var((0, 2, 3), unbiased=False)
-    assert ((mean - zd.mean((0, 2, 3))).abs() / zd.mean((0, 2, 3)).abs()).max().item() < 1e-6
+    assert ((mean - zd.mean((0, 2, 3))).abs() / zd.mean((0, 2, 3)).abs()).max().item() < 1e-5
     assert ((istd - 1 / (var + 1e-3).sqrt()).abs() * (var + 1e-3).sqrt()).max().item() < 1e-4
+
+
+def _flat(st, cnt):
+    """the conv_fwd helper's statistics views -> their (contiguous) workspace"""
+    base = st.reshape(-1)
+    assert cnt.data_ptr() == base.data_ptr() + base.numel() * 4
+    return torch.as_strided(base, (base.numel() + cnt.numel(),), (1,))

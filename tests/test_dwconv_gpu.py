@@ -9,7 +9,7 @@ import pytest
 import torch
 import torch.nn.functional as F
 
-from hiputil import DT, check_moments, nchw, nhwc, r8
+from hiputil import DT, check_moments, nchw, nhwc, r8, split_stats, stats_buffer
 from yms import _lib as L
 
 pytestmark = pytest.mark.gpu
@@ -51,15 +51,12 @@ def test_dwconv_fwd_dgrad_wgrad(shp, dt):
     assert y[..., :16].abs().max().item() == 0
     # train: z + BN partial statistics
     rows = L.lib().yms_dwconv_stats_rows(sp)
-    stt = torch.full((rows, 2, r8(c)), float("nan"), device="cuda")
+    buf = stats_buffer(rows, r8(c))
     y2 = torch.zeros((n, h, w, r8(c)), dtype=dtype, device="cuda")
     L.call("yms_dwconv_fwd", sp, xb.data_ptr(), xb.shape[-1], 8, wd.data_ptr(), y2.data_ptr(), y2.shape[-1], 0,
-           None, None, 0, stt.data_ptr(), r8(c), st)
+           None, None, 0, buf.data_ptr(), r8(c), st)
     _close(nchw(y2, c).cpu(), z, TOL[dt])
-    counts = torch.empty(rows)
-    L.call("yms_dwconv_stats_counts", sp, counts.data_ptr())
-    assert counts.sum().item() == n * h * w
-    check_moments(stt, z, 1e-4 if dt == "f32" else 1e-3, counts)
+    check_moments(split_stats(buf, rows, r8(c)), z, 1e-4 if dt == "f32" else 1e-3)
     # backward
     dz = torch.randn(n, c, h, w, generator=g)
     xg = xr.clone().requires_grad_(True)

@@ -46,7 +46,7 @@ for (n, h, w, ci, co, k, s_) in SHAPES:
     y = torch.empty(n, sh.ho, sh.wo, r8(co), device="cuda", dtype=dt)
     sc = torch.ones(co, device="cuda"); sf = torch.zeros(co, device="cuda")
     rows, ld = L.lib().yms_conv_stats_rows(sp), L.lib().yms_conv_stats_ld(sp)
-    stt = torch.empty(rows * 2 * ld, device="cuda")
+    stt = torch.empty(rows * (2 * ld + 1), device="cuda")
     dz = torch.randn(n, sh.ho, sh.wo, r8(co), device="cuda").to(dt)
     dx = torch.empty_like(x)
     wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)

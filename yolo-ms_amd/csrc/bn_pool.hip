@@ -39,95 +39,123 @@ __global__ void bn_fold_kernel(int c, const float* g, const float* b, const floa
 }
 
 // Statistics rows (conv_common.hpp contract): row r = (sum z, sum (z - mean_r)^2) over n_r
-// pixels, n_r = counts[r] when a count table is given (depthwise tiles), else the 128-pixel
-// rule min(128, count - 128 r) of the NT convolutions.  Rows are merged with Chan's pairwise
-// update, M2 = sum_r [M2_r + n_r (mean_r - mean)^2], in fp64 -- no sum z^2 - n mean^2
-// cancellation anywhere.
-__device__ __forceinline__ double stats_row_n(int r, const float* counts, long count) {
-  return counts ? (double)counts[r] : (double)min(128l, count - 128l * r);
-}
+// pixels, n_r = counts[r] (the producers write the count table right after the rows; rows with
+// n_r = 0 are skipped).  Rows are merged in ONE pass in fp64 with the shifted-data form of
+// Chan's update: with K = the first row's mean (a sample of the data, so |mean - K| is of the
+// order of the spread),  M2 = sum_r [M2_r + n_r (m_r - K)^2] - (sum_r n_r (m_r - K))^2 / N,
+// free of the sum z^2 - n mean^2 cancellation.  Row means m_r are formed in fp32 (the
+// producers' own precision).
+struct Moments {           // n, sum n_r (m_r - K), sum [M2_r + n_r (m_r - K)^2] about the shift K
+  double n = 0.0, d1 = 0.0, d2 = 0.0, K = 0.0;
+  __device__ void add_row(float s1, float m2, float nr) {
+    if (!(nr > 0.f)) return;
+    const float mr = s1 / nr;
+    if (n == 0.0) K = (double)mr;
+    const double d = (double)mr - K;
+    n += nr;
+    d1 += nr * d;
+    d2 += (double)m2 + nr * d * d;
+  }
+  __device__ void merge(const Moments& o) {      // re-centre o on this K, then add
+    if (o.n == 0.0) return;
+    if (n == 0.0) { *this = o; return; }
+    const double e = o.K - K;
+    n += o.n;
+    d1 += o.d1 + o.n * e;
+    d2 += o.d2 + 2.0 * e * o.d1 + o.n * e * e;
+  }
+  __device__ double sum() const { return d1 + n * K; }
+  __device__ double m2() const { return n > 0.0 ? d2 - d1 * d1 / n : 0.0; }
+  __device__ void store(double (*red)[4], int i) const { red[i][0] = n; red[i][1] = d1; red[i][2] = d2; red[i][3] = K; }
+  __device__ static Moments load(const double (*red)[4], int i) {
+    Moments m;
+    m.n = red[i][0]; m.d1 = red[i][1]; m.d2 = red[i][2]; m.K = red[i][3];
+    return m;
+  }
+};
 
 // Pre-reduction for long statistics tables: block (cb, s) merges rows [s*R, (s+1)*R) of
 // channels [64cb, 64cb+64) and stores the merged (sum, M2) over row s*R -- the first row of its
-// own range, so no block reads a row another block writes.  256 threads = 64 channels x 4 lanes.
-__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int c, float* stats, int rows, int ld, int R,
-                                                               const float* counts, long count) {
-  __shared__ double red[3][4][64];
+// own range, so no block reads a row another block writes (the count table is left as it is:
+// the finalize sums the counts of each merged range).  256 threads = 64 channels x 4 lanes, two
+// rows in flight per lane.
+__global__ __launch_bounds__(256) void bn_stats_partial_kernel(int c, float* stats, int rows, int ld, int R) {
+  __shared__ double red[4 * 64][4];
   const int tx = threadIdx.x & 63, ty = threadIdx.x >> 6;
   const int ch = blockIdx.x * 64 + tx;
   const int r0 = blockIdx.y * R, r1 = min(rows, r0 + R);
-  double a1 = 0.0, an = 0.0;
-  if (ch < c)
-    for (int r = r0 + ty; r < r1; r += 4) {
-      a1 += stats[(long)r * 2 * ld + ch];
-      an += stats_row_n(r, counts, count);
+  const float* cnt = stats + (long)rows * 2 * ld;
+  const float* s1p = stats + ch;
+  const float* m2p = stats + ld + ch;
+  const long rs = 2l * ld;
+  Moments a, b;
+  if (ch < c) {
+    int r = r0 + ty;
+    for (; r + 4 < r1; r += 8) {
+      a.add_row(s1p[r * rs], m2p[r * rs], cnt[r]);
+      b.add_row(s1p[(r + 4) * rs], m2p[(r + 4) * rs], cnt[r + 4]);
     }
-  red[0][ty][tx] = a1;
-  red[1][ty][tx] = an;
-  __syncthreads();
-  const double t1 = (red[0][0][tx] + red[0][1][tx]) + (red[0][2][tx] + red[0][3][tx]);
-  const double tn = (red[1][0][tx] + red[1][1][tx]) + (red[1][2][tx] + red[1][3][tx]);
-  const double mu = tn > 0.0 ? t1 / tn : 0.0;
-  double a2 = 0.0;
-  if (ch < c)
-    for (int r = r0 + ty; r < r1; r += 4) {
-      const double n = stats_row_n(r, counts, count);
-      const double d = (double)stats[(long)r * 2 * ld + ch] / n - mu;
-      a2 += (double)stats[(long)r * 2 * ld + ld + ch] + n * d * d;
-    }
-  red[2][ty][tx] = a2;
+    if (r < r1) a.add_row(s1p[r * rs], m2p[r * rs], cnt[r]);
+    a.merge(b);
+  }
+  a.store(red, ty * 64 + tx);
   __syncthreads();
   if (ty == 0 && ch < c) {
-    const double t2 = (red[2][0][tx] + red[2][1][tx]) + (red[2][2][tx] + red[2][3][tx]);
-    stats[(long)r0 * 2 * ld + ch] = (float)t1;
-    stats[(long)r0 * 2 * ld + ld + ch] = (float)t2;
+    Moments t = Moments::load(red, tx);
+    for (int k = 1; k < 4; ++k) t.merge(Moments::load(red, k * 64 + tx));
+    stats[(long)r0 * rs + ch] = (float)t.sum();
+    stats[(long)r0 * rs + ld + ch] = (float)t.m2();
   }
 }
 
-// pixels of merged row k (rows [k*rs, min(rows_total, (k+1)*rs)) of the original table)
-__device__ __forceinline__ double merged_row_n(int k, int rs, int rows_total, const float* counts, long count) {
-  if (!counts) return (double)min((long)rs * 128l, count - (long)k * rs * 128l);
-  double n = 0.0;
-  for (int r = k * rs, e = min(rows_total, (k + 1) * rs); r < e; ++r) n += (double)counts[r];
-  return n;
-}
-
-// rows are read at stride rs (rs > 1 after bn_stats_partial_kernel); 32 channels x 32 row-lanes
-// per block (1024 threads); two passes: the mean from the row sums, then the merged M2
+// rows are read at stride rs (rs > 1 after bn_stats_partial_kernel; merged row k covers original
+// rows [k*rs, min(rows_total, (k+1)*rs)), its count the sum of theirs); FIN_CW channels x FIN_RL
+// row lanes per block (1024 threads: short tables are latency-bound, so many lanes with few
+// rows each), one shifted pass per lane, fixed-order tree combine
+constexpr int FIN_CW = 8, FIN_RL = 1024 / FIN_CW;
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* stats, int rows, int ld, int rs,
-                                                           int rows_total, const float* counts, long count,
-                                                           const float* g, const float* b, float* rm, float* rv,
-                                                           float momentum, float eps, float* mi, float* scale,
-                                                           float* shift) {
-  __shared__ double red[32][33];
-  __shared__ double mean_s[32];
-  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
-  const int ch = blockIdx.x * 32 + tx;
-  double a1 = 0.0;
-  if (ch < c)
-    for (int r = ty; r < rows; r += 32) a1 += stats[(long)r * rs * 2 * ld + ch];
-  red[ty][tx] = a1;
-  __syncthreads();
-  if (ty == 0) {
-    double t1 = 0.0;
-    for (int k = 0; k < 32; ++k) t1 += red[k][tx];
-    mean_s[tx] = t1 / (double)count;
-  }
-  __syncthreads();
-  const double mean = mean_s[tx];
-  double a2 = 0.0;
-  if (ch < c)
-    for (int r = ty; r < rows; r += 32) {
-      const double n = merged_row_n(r, rs, rows_total, counts, count);
-      const double d = (double)stats[(long)r * rs * 2 * ld + ch] / n - mean;
-      a2 += (double)stats[(long)r * rs * 2 * ld + ld + ch] + n * d * d;
+                                                           int rows_total, long count, const float* g,
+                                                           const float* b, float* rm, float* rv, float momentum,
+                                                           float eps, float* mi, float* scale, float* shift) {
+  __shared__ double red[FIN_RL * (FIN_CW + 1)][4];
+  const int tx = threadIdx.x % FIN_CW, ty = threadIdx.x / FIN_CW;
+  const int ch = blockIdx.x * FIN_CW + tx;
+  const float* cnt = stats + (long)rows_total * 2 * ld;
+  Moments a;
+  if (ch < c) {
+    if (rs == 1) {
+      // four rows per iteration, every load issued before the first use
+      int r = ty;
+      for (; r + 3 * FIN_RL < rows; r += 4 * FIN_RL) {
+        float s1[4], m2[4], n[4];
+#pragma unroll
+        for (int u = 0; u < 4; ++u) {
+          s1[u] = stats[(long)(r + FIN_RL * u) * 2 * ld + ch];
+          m2[u] = stats[(long)(r + FIN_RL * u) * 2 * ld + ld + ch];
+          n[u] = cnt[r + FIN_RL * u];
+        }
+#pragma unroll
+        for (int u = 0; u < 4; ++u) a.add_row(s1[u], m2[u], n[u]);
+      }
+      for (; r < rows; r += FIN_RL) a.add_row(stats[(long)r * 2 * ld + ch], stats[(long)r * 2 * ld + ld + ch], cnt[r]);
+    } else {
+      for (int r = ty; r < rows; r += FIN_RL) {
+        float n = 0.f;   // integer-valued: exact in fp32 below 2^24 pixels per merged row
+        for (int q = r * rs, e = min(rows_total, (r + 1) * rs); q < e; ++q) n += cnt[q];
+        a.add_row(stats[(long)r * rs * 2 * ld + ch], stats[(long)r * rs * 2 * ld + ld + ch], n);
+      }
     }
-  red[ty][tx] = a2;   // pass-1 partials were consumed before the barrier above
-  __syncthreads();
+  }
+  // fixed-order tree over the row lanes: lane ty absorbs lane ty + h
+  for (int h = FIN_RL / 2; h >= 1; h >>= 1) {
+    if (ty >= h && ty < 2 * h) a.store(red, ty * (FIN_CW + 1) + tx);
+    __syncthreads();
+    if (ty < h) a.merge(Moments::load(red, (ty + h) * (FIN_CW + 1) + tx));
+    __syncthreads();
+  }
   if (ty == 0 && ch < c) {
-    double t2 = 0.0;
-    for (int k = 0; k < 32; ++k) t2 += red[k][tx];
-    const double var = t2 / (double)count;
+    const double mean = a.n > 0.0 ? a.sum() / a.n : 0.0;
+    const double var = fmax(a.m2(), 0.0) / (double)count;
     const float invstd = (float)(1.0 / sqrt(var + (double)eps));
     const double uvar = count > 1 ? var * (double)count / (double)(count - 1) : var;
     if (rm) rm[ch] = (float)((1.0 - momentum) * (double)rm[ch] + momentum * mean);
@@ -730,25 +758,24 @@ yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float
   return launch_status();
 }
 
-yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count, const float* row_counts,
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream) {
   if (c <= 0 || !stats || rows <= 0 || count <= 0 || !gamma || !beta || !mean_invstd || !scale || !shift)
     return YMS_ERR_INVALID;
   if (stats_ld < c) return YMS_ERR_INVALID;
-  if (!row_counts && (count > 128l * rows || count <= 128l * (rows - 1))) return YMS_ERR_INVALID;
   int rs = 1, nrows = rows;
-  if (rows > 256) {   // long tables: pre-reduce in parallel (in place), then finalize the partial rows
+  if (rows > 1024) {   // long tables: pre-reduce in parallel (in place), then finalize the partial rows
     const int S = std::min(256, cdiv(rows, 64));
     rs = cdiv(rows, S);
     nrows = cdiv(rows, rs);
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(cdiv(c, 64), nrows), dim3(256), 0, (hipStream_t)stream, c,
-                       stats, rows, stats_ld, rs, row_counts, count);
+                       stats, rows, stats_ld, rs);
   }
-  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c,
-                     (const float*)stats, nrows, stats_ld, rs, rows, row_counts, count, gamma, beta, rmean, rvar,
-                     momentum, eps, mean_invstd, scale, shift);
+  hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, FIN_CW)), dim3(1024), 0, (hipStream_t)stream, c,
+                     (const float*)stats, nrows, stats_ld, rs, rows, count, gamma, beta, rmean, rvar, momentum,
+                     eps, mean_invstd, scale, shift);
   return launch_status();
 }
 

@@ -84,24 +84,38 @@ constexpr int NT_RSRC3 = 0x00020000;        // buffer descriptor word 3 (gfx9 ra
 // the registers, combined across the two lane halves.
 template <int TM, typename Acc>
 __device__ __forceinline__ void wave_col_moments(const Acc& acc, int b, int nw, int lh, float& s1, float& m2) {
-  const bool full = nw >= TM * 32;
-  float s = 0.f;
+  float s = 0.f, q = 0.f;
+  if (nw >= TM * 32) {                    // wave-uniform: every row valid, no per-element selects
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (full || a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh < nw) s += acc[a][b][i];
-  s += __shfl_xor(s, 32);
-  const float mu = nw > 0 ? s / (float)nw : 0.f;
-  float q = 0.f;
+      for (int i = 0; i < 16; ++i) s += acc[a][b][i];
+    s += __shfl_xor(s, 32);
+    const float mu = s * (1.0f / (TM * 32));
 #pragma unroll
-  for (int a = 0; a < TM; ++a)
+    for (int a = 0; a < TM; ++a)
 #pragma unroll
-    for (int i = 0; i < 16; ++i)
-      if (full || a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh < nw) {
+      for (int i = 0; i < 16; ++i) {
         const float d = acc[a][b][i] - mu;
         q += d * d;
       }
+  } else {
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh < nw) s += acc[a][b][i];
+    s += __shfl_xor(s, 32);
+    const float mu = nw > 0 ? s / (float)nw : 0.f;
+#pragma unroll
+    for (int a = 0; a < TM; ++a)
+#pragma unroll
+      for (int i = 0; i < 16; ++i)
+        if (a * 32 + (i & 3) + 8 * (i >> 2) + 4 * lh < nw) {
+          const float d = acc[a][b][i] - mu;
+          q += d * d;
+        }
+  }
   q += __shfl_xor(q, 32);
   s1 = s;
   m2 = q;

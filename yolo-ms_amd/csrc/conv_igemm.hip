@@ -33,6 +33,7 @@ struct NTParams {
   int res_ld, res_off;
   float* stats;
   int stats_ld;
+  float* stats_cnt; // per-row pixel counts (right after the rows, conv_common.hpp contract)
   int SH, SW;       // source spatial dims
   int OW;           // row-space width
   int stride, pad;
@@ -397,6 +398,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
       float* so = p.stats + (long)tile_m * 2 * p.stats_ld;
       so[n0 + tid] = t1;
       so[p.stats_ld + n0 + tid] = t2;
+      if (tile_n == 0 && tid == 0) p.stats_cnt[tile_m] = (float)nrow;
     }
   }
 }
@@ -422,14 +424,19 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
   constexpr bool B_PART = BN < RPP;                         // only the first BN/8 waves load B
   constexpr int B_SLOTS = B_PART ? 1 : BN / RPP;
   constexpr int STAGE = (BM + BN) * 128;
-  constexpr int RED = (EPI == EPI_STATS) ? WGM * 2 * BN * 4 : 0;
+  // statistics: per-wave column partials [WGM][2][BN] + the combiner threads' running moments
+  // [3][SROWS*BN] (kept in LDS: three more live VGPRs would cost a block per CU)
+  constexpr int RED = (EPI == EPI_STATS) ? (WGM * 2 + 3 * (BM / 128 > 0 ? BM / 128 : 1)) * BN * 4 : 0;
   constexpr int PRM = (EPI == EPI_AFFINE) ? 2 * NTP_MAX_AFFINE_COLS * 4 : 0;
   static_assert((B_PART || BN % RPP == 0) && BM % RPP == 0 && BN <= NTHR, "tile");
   // the output tile is staged through the ring stage just consumed, in NH passes of HR rows
   constexpr int NH = (BM * BN * (int)sizeof(T) > STAGE) ? 2 : 1;
   constexpr int HR = BM / NH;
   static_assert(HR * BN * (int)sizeof(T) <= STAGE && HR % (BM / WGM) == 0, "staging must fit one ring stage");
-  // BN statistics: one [2][ld] row per 128 output rows (yms_conv_stats_rows), whatever BM is
+  // BN statistics: every block walks tiles of ONE column tile (the grid is a multiple of tiles_n),
+  // so it keeps per-column running moments of its tiles (Chan merges, in the combiner threads'
+  // registers) and writes one row per 128-row half of its tiles, slot lb / tiles_n, at the end
+  // (yms_conv_stats_rows = SROWS x grid / tiles_n, counts after the rows)
   constexpr int SROWS = BM / 128 > 0 ? BM / 128 : 1;
   static_assert(BM % 128 == 0 && WGM % SROWS == 0, "statistics rows");
   __shared__ __attribute__((aligned(16))) char smem[ST * STAGE + RED + PRM + 16];
@@ -627,6 +634,15 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
     __builtin_amdgcn_s_waitcnt((0xF) | (3 << 14) | (0x7 << 4) | (0 << 8));   // lgkmcnt(0) only
     raw_barrier();
   };
+  // combiner thread (sr, c) = tid < BN*SROWS owns running-moment slot tid (n, sum, M2)
+  float* const run = red + WGM * 2 * BN;
+  if constexpr (EPI == EPI_STATS) {
+    if (tid < BN * SROWS) {
+      run[tid] = 0.f;
+      run[BN * SROWS + tid] = 0.f;
+      run[2 * BN * SROWS + tid] = 0.f;
+    }
+  }
   auto epilogue = [&](int t, int stage) {
     const int tile_m = t / p.tiles_n, m0 = tile_m * BM, n0 = (t % p.tiles_n) * BN;
     T* stg = reinterpret_cast<T*>(smem + stage * STAGE);
@@ -687,14 +703,25 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
         if (h == 0 && tid < BN * SROWS) {
           const int sr = tid / BN, c = tid - sr * BN;
           constexpr int WPR = WGM / SROWS;    // wave rows per statistics row
-          const int srow = tile_m * SROWS + sr;
-          float t1, t2;
-          merge_moments<WPR, WTM>(red + (sr * WPR * 2 + 0) * BN + c, red + (sr * WPR * 2 + 1) * BN + c, 2 * BN,
-                                  M - srow * 128, t1, t2);
-          if (srow * 128 < M) {
-            float* so = p.stats + (long)srow * 2 * p.stats_ld;
-            so[n0 + c] = t1;
-            so[p.stats_ld + n0 + c] = t2;
+          const int r0 = m0 + sr * 128;
+          const int nt = min(128, max(0, M - r0));
+          if (nt > 0) {
+            float t1, t2;
+            merge_moments<WPR, WTM>(red + (sr * WPR * 2 + 0) * BN + c, red + (sr * WPR * 2 + 1) * BN + c, 2 * BN,
+                                    nt, t1, t2);
+            const float rn = run[tid];
+            if (rn == 0.f) {
+              run[tid] = (float)nt;
+              run[BN * SROWS + tid] = t1;
+              run[2 * BN * SROWS + tid] = t2;
+            } else {
+              const float rs = run[BN * SROWS + tid];
+              const float nn = rn + (float)nt;
+              const float d = t1 / (float)nt - rs / rn;
+              run[2 * BN * SROWS + tid] += t2 + d * d * (rn * (float)nt / nn);
+              run[BN * SROWS + tid] = rs + t1;
+              run[tid] = nn;
+            }
           }
         }
       }
@@ -754,6 +781,16 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
       ctile += G;
     }
     if (++stage == ST) stage = 0;
+  }
+  if constexpr (EPI == EPI_STATS) {
+    if (tid < BN * SROWS) {
+      const int sr = tid / BN, c = tid - sr * BN;
+      const int row = (lb / p.tiles_n) * SROWS + sr, n0 = (lb % p.tiles_n) * BN;
+      float* so = p.stats + (long)row * 2 * p.stats_ld;
+      so[n0 + c] = run[BN * SROWS + tid];
+      so[p.stats_ld + n0 + c] = run[2 * BN * SROWS + tid];
+      if (n0 == 0 && c == 0) p.stats_cnt[row] = run[tid];
+    }
   }
 }
 
@@ -1190,45 +1227,67 @@ static TileChoice choose_tile(int ncols) {
 
 static int cu_count() { return conv_cu_count(); }
 
-// persistent grid: at most two resident blocks per CU (the kernels are sized for 2/CU);
+static int env_int(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+// YMS_NT_VARIANT = 6 (dev A/B): 256-row tiles of 16 waves at 1 block per CU (25% fewer LDS-fill
+// bytes per FLOP, 2 k-tiles in flight).  YMS_NT_DGRAD_MULT / YMS_NT_FWD_MULT = m launch OCC x CUs x m
+// persistent blocks (dev A/B).  Read once per process.
+static int nt_variant() { static const int v = env_int("YMS_NT_VARIANT", 0); return v; }
+static int nt_fwd_mult() { static const int v = std::max(1, env_int("YMS_NT_FWD_MULT", 1)); return v; }
+static int nt_dgrad_mult() { static const int v = std::max(1, env_int("YMS_NT_DGRAD_MULT", 1 << 16)); return v; }
+
+struct NtpGeo { int bm, bn, occ; };
+static NtpGeo ntp_geo(int cfg) {
+  const bool v6 = nt_variant() == 6;
+  if (cfg == 0) return v6 ? NtpGeo{256, 128, 1} : NtpGeo{128, 128, 2};
+  if (cfg == 1) return v6 ? NtpGeo{256, 64, 1} : NtpGeo{128, 64, 3};
+  return NtpGeo{256, 32, 2};
+}
+
+// persistent grid: OCC resident blocks per CU (x mult), at most one block per tile.  Statistics
+// launches round it down to a multiple of tiles_n, so every block walks tiles of one column tile
+// (conv_ntp_kernel's per-block statistics slots).
+static long ntp_grid(long M, int tiles_n, int bm, long occ_blocks_per_cu, bool stats) {
+  const long ntiles = (long)cdiv(M, bm) * tiles_n;
+  long g = std::max<long>(1, std::min<long>(ntiles, occ_blocks_per_cu * cu_count()));
+  if (stats) g = std::max<long>(tiles_n, g - g % tiles_n);
+  return g;
+}
+
 // p.M is the largest parity class for DGRAD2
 template <typename K>
-static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, hipStream_t st, int occ, int nthr) {
-  const long ntiles = (long)cdiv(p.M, bm) * p.tiles_n;
-  const unsigned gx = (unsigned)std::max<long>(1, std::min<long>(ntiles, (long)occ * cu_count()));
+static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, hipStream_t st, long occ, int nthr,
+                              bool stats) {
+  const unsigned gx = (unsigned)ntp_grid(p.M, p.tiles_n, bm, occ, stats);
   hipLaunchKernelGGL(kernel, dim3(gx, gy), dim3(nthr), 0, st, p);
 }
 
 template <typename T, int KS, int MODE, int EPI, bool UNI>
 static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st) {
   NTParams p = p0;
-  static const int variant = getenv("YMS_NT_VARIANT") ? atoi(getenv("YMS_NT_VARIANT")) : 0;
   // dgrad grids: one block per output tile by default.  The weight gradients run beside dgrad on
   // the side stream, and persistent blocks that start late on CUs the wgrad kernels hold would
   // each still owe their fixed share of tiles (interleaved A/B: 19.91 -> 19.74 ms/step).
-  // YMS_NT_DGRAD_MULT = m launches OCC x CUs x m persistent blocks instead (dev A/B; m = 1 is
-  // the persistent grid).
-  static const int dmult = getenv("YMS_NT_DGRAD_MULT") ? std::max(1, atoi(getenv("YMS_NT_DGRAD_MULT"))) : 1 << 16;
-  static const int fmult = getenv("YMS_NT_FWD_MULT") ? std::max(1, atoi(getenv("YMS_NT_FWD_MULT"))) : 1;
-  const int mult = MODE == MODE_FWD ? fmult : dmult;
+  const long mult = MODE == MODE_FWD ? nt_fwd_mult() : nt_dgrad_mult();
+  const bool stats = EPI == EPI_STATS;
+  const NtpGeo g = ntp_geo(cfg);
+  p.tiles_n = cdiv(p.Ncols, g.bn);
   // 8-wave blocks at 2-3 per CU (4-6 waves per SIMD) hide the ds_read -> MFMA and barrier
-  // latencies that 4-wave blocks expose; variant 6 (dev A/B): 256-row tiles of 16 waves at
-  // 1 block per CU (25% fewer LDS-fill bytes per FLOP, 2 k-tiles in flight).
+  // latencies that 4-wave blocks expose
   if (cfg == 0) {
-    p.tiles_n = cdiv(p.Ncols, 128);
-    if (variant == 6)
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1>, p, 256, gy, st, 1 * mult, 1024);
+    if (g.bm == 256)
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1>, p, 256, gy, st, g.occ * mult, 1024, stats);
     else
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, 2 * mult, 512);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, g.occ * mult, 512, stats);
   } else if (cfg == 1) {
-    p.tiles_n = cdiv(p.Ncols, 64);
-    if (variant == 6)
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 64, 8, 2, 3, UNI, 1>, p, 256, gy, st, 1 * mult, 1024);
+    if (g.bm == 256)
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 64, 8, 2, 3, UNI, 1>, p, 256, gy, st, g.occ * mult, 1024, stats);
     else
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, 3 * mult, 512);
+      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, g.occ * mult, 512, stats);
   } else {
-    p.tiles_n = cdiv(p.Ncols, 32);
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, 2 * mult, 512);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, g.occ * mult, 512, stats);
   }
 }
 
@@ -1285,7 +1344,6 @@ static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hip
   return launch_status();
 }
 
-static int rows_for(int M, int cfg) { (void)cfg; return cdiv(M, 128); }
 
 struct WgradPlan {
   int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc, kp, var;
@@ -1447,8 +1505,11 @@ yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* p
 
 int yms_conv_stats_rows(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
-  TileChoice tc = choose_tile(s->cout);
-  return rows_for(s->n * s->ho * s->wo, tc.cfg);
+  const long M = (long)s->n * s->ho * s->wo;
+  if (s->dtype == YMS_F32) return (int)cdiv(M, 128);     // conv_nt_kernel: one row per 128-row tile
+  const NtpGeo g = ntp_geo(choose_tile(s->cout).cfg);    // conv_ntp_kernel: one slot per block
+  const int tiles_n = cdiv(s->cout, g.bn);
+  return (int)(ntp_grid(M, tiles_n, g.bm, (long)g.occ * nt_fwd_mult(), true) / tiles_n) * (g.bm / 128);
 }
 int yms_conv_stats_ld(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
@@ -1479,6 +1540,7 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   p.res = (const char*)res; p.res_ld = res_ld; p.res_off = res_off;
   p.stats = stats;
   p.stats_ld = (int)rup(s->cout, 128);
+  if (stats) p.stats_cnt = stats + (long)yms_conv_stats_rows(s) * 2 * p.stats_ld;
   p.SH = s->h; p.SW = s->w; p.OW = s->wo;
   if (!offsets32(s->n, s->h, s->w, x_ld)) return YMS_ERR_UNSUPPORTED;
   p.stride = s->stride; p.pad = s->pad;

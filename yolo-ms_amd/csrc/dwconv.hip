@@ -36,6 +36,7 @@ struct DwParams {
   int act;
   float* stats;
   int stats_ld;
+  float* stats_cnt;      // per-tile pixel counts, right after the rows
   int accumulate;
   int N, H, W, C;
   int tiles_x, tiles_y;  // spatial tiles per image
@@ -150,9 +151,9 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
     }
   }
   if (MODE == DW_FWD_STATS) {
-    // one statistics row per spatial tile (conv_common.hpp contract, row counts from
-    // yms_dwconv_stats_counts): sum and centred M2 over the tile's valid pixels, two passes over
-    // the fp32 accumulators, wave butterflies in a fixed order
+    // one statistics row per spatial tile (conv_common.hpp contract; its pixel count goes to the
+    // count table after the rows): sum and centred M2 over the tile's valid pixels, two passes
+    // over the fp32 accumulators, wave butterflies in a fixed order
     const int vy = min(DW_TY, p.H - y0), vx = min(DW_TX, p.W - x0);
     const float inv_n = 1.0f / (float)(vy * vx);
     float s1[8], m2[8];
@@ -190,6 +191,7 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
       so[c + lane] = a;
       so[p.stats_ld + c + lane] = b;
     }
+    if (blockIdx.y == 0 && threadIdx.x == 0) p.stats_cnt[tile] = (float)(vy * vx);
   }
 }
 
@@ -352,18 +354,6 @@ int yms_dwconv_stats_rows(const yms_dw_shape* s) {
   return dw_tiles(s, tx, ty);
 }
 
-yms_status yms_dwconv_stats_counts(const yms_dw_shape* s, float* counts) {
-  if (!dw_shape_ok(s) || !counts) return YMS_ERR_INVALID;
-  int tx, ty;
-  const int rows = dw_tiles(s, tx, ty);
-  for (int r = 0; r < rows; ++r) {
-    const int rem = r % (tx * ty);
-    const int y0 = (rem / tx) * DW_TY, x0 = (rem % tx) * DW_TX;
-    counts[r] = (float)(std::min(DW_TY, s->h - y0) * std::min(DW_TX, s->w - x0));
-  }
-  return YMS_OK;
-}
-
 yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
                           int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
                           int stats_ld, void* stream) {
@@ -374,6 +364,7 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   p.src = (const char*)x; p.src_ld = x_ld; p.src_off = x_off; p.w = w;
   p.dst = (char*)y; p.dst_ld = y_ld; p.dst_off = y_off;
   p.scale = scale; p.shift = shift; p.act = act; p.stats = stats; p.stats_ld = stats_ld;
+  if (stats) p.stats_cnt = stats + (long)yms_dwconv_stats_rows(s) * 2 * stats_ld;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
   const int tiles = dw_tiles(s, p.tiles_x, p.tiles_y);
   dim3 grid((unsigned)tiles, (unsigned)((s->c + DW_CB - 1) / DW_CB));

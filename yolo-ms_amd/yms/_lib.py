@@ -65,7 +65,7 @@ _SIGS = {
     "yms_conv_wgrad_ws_bytes": (_SZ, [_SP]),
     "yms_conv_wgrad": (_I, [_SP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
     "yms_bn_fold": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
-    "yms_bn_finalize": (_I, [_I, _P, _I, _I, _L, _P, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P]),
+    "yms_bn_finalize": (_I, [_I, _P, _I, _I, _L, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P]),
     "yms_affine_act": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _I, _I, _P]),
     "yms_bn_bwd_rows": (_I, [_L, _I]),
     "yms_bn_act_bwd_reduce": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
@@ -87,7 +87,6 @@ _SIGS = {
     "yms_zero": (_I, [_P, _SZ, _P]),
     "yms_copy": (_I, [_P, _P, _SZ, _P]),
     "yms_dwconv_stats_rows": (_I, [_DP]),
-    "yms_dwconv_stats_counts": (_I, [_DP, _P]),
     "yms_dwconv_fwd": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
     "yms_dwconv_dgrad": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
     "yms_dwconv_wgrad_ws_bytes": (_SZ, [_DP]),

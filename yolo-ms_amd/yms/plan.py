@@ -218,15 +218,11 @@ class ConvOp:
             self.mi = La.alloc(8 * c)
             self.stats_rows = L.lib().yms_conv_stats_rows(self.sp)
             self.stats_ld = L.lib().yms_conv_stats_ld(self.sp)
-            plan.need_scratch("stats", 4 * 2 * self.stats_rows * self.stats_ld)
+            plan.need_scratch("stats", 4 * self.stats_rows * (2 * self.stats_ld + 1))
             plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
             plan.need_scratch("coef", 8 * c)
             self.cnt = plan.counter()
             plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
-
-    def row_counts(self):
-        """Pixels per BN statistics row: None = the convolutions' 128-pixel rows."""
-        return None
 
     def pack_specs(self):
         """(shape, fp32 weight, arena byte offset of the packed copy, for_dgrad) per training pack."""
@@ -260,8 +256,7 @@ class ConvOp:
         L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
                None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
         bn = m.bn
-        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, self.row_counts(),
-               bn.weight.data_ptr(),
+        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
@@ -415,20 +410,11 @@ class DWConvOp(ConvOp):
             self.mi = La.alloc(8 * c)
             self.stats_rows = L.lib().yms_dwconv_stats_rows(self.sp)
             self.stats_ld = r8(c)
-            plan.need_scratch("stats", 4 * 2 * self.stats_rows * self.stats_ld)
+            plan.need_scratch("stats", 4 * self.stats_rows * (2 * self.stats_ld + 1))
             plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
             plan.need_scratch("coef", 8 * c)
             plan.need_scratch("wgrad", L.lib().yms_dwconv_wgrad_ws_bytes(self.sp))
             self.cnt = plan.counter()
-            counts = torch.empty(self.stats_rows, dtype=torch.float32)
-            L.call("yms_dwconv_stats_counts", self.sp, counts.data_ptr())
-            self.counts_host, self.counts_dev = counts, None
-
-    def row_counts(self):
-        """Pixels per statistics row (one 8x32 tile each): a static table, uploaded once."""
-        if self.counts_dev is None:
-            self.counts_dev = self.counts_host.to(torch.device("cuda", torch.cuda.current_device()))
-        return self.counts_dev.data_ptr()
 
     def pack_specs(self):
         return []
@@ -452,8 +438,7 @@ class DWConvOp(ConvOp):
         L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, base + self.z, self.zld, 0, None, None,
                L.ACT_NONE, stats, self.stats_ld, rt.st)
         bn = self.mod.bn
-        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, self.row_counts(),
-               bn.weight.data_ptr(),
+        L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
