@@ -219,6 +219,21 @@ yms_status yms_map_accumulate(int n_det, const float* scores, const int* labels,
                               const uint8_t* tp, const uint8_t* kept, int n_classes, const int* n_gt,
                               double* ap, double* map);
 
+/* ---- detection loss ------------------------------------------------------- */
+/* The reference's ComputeLoss (yolov8/tools/loss.py:94-677; python binding
+ * yolov8.tools.loss.ComputeLoss mirrors its constructor and call) on the raw training head maps:
+ * maps[l] / grads[l] are NHWC [batch, hs[l], ws_[l], ld] (64 DFL logits, then nc class logits;
+ * grads NULL = value only, grads[l] written in full for channels < 64 + nc).  targets: device fp32
+ * [n_targets][6] = (image, class, cx, cy, w, h) normalised; boxes scale by (img_w, img_h).
+ * iou_type 0 iou, 1 giou, 2 diou, 3 ciou.  pos_weight: NULL or device fp32 [nc].  lambdas (host):
+ * box, cls, dfl gains (7.5, 0.5, 1.5 in the reference).  out (device fp32 [4]) = total, box, cls,
+ * dfl; grads = d(total)/d(maps).  ws: yms_det_loss_ws_bytes() bytes of device scratch. */
+size_t yms_det_loss_ws_bytes(int batch, int anchors, int nc, int n_targets);
+yms_status yms_det_loss(int dtype, int batch, int nc, int nlevels, const void* const* maps, void* const* grads,
+                        const int* hs, const int* ws_, const float* strides, int ld, const float* targets,
+                        int n_targets, float img_w, float img_h, int iou_type, const float* pos_weight,
+                        const float* lambdas, void* ws, size_t ws_bytes, float* out, void* stream);
+
 /* ---- head decode + NMS ------------------------------------------------------------------- */
 /* Raw head maps lvl[i]: NHWC [n, h_i, w_i, no_ld] with channels (64 DFL box logits, nc cls
  * logits).  out: [n, A, 4+nc] fp32 = (cx, cy, w, h)*stride_i, sigmoid(cls).  When nms_score
