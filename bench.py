@@ -42,6 +42,10 @@ def parse():
     ap.add_argument("--nc", type=int, default=80)
     ap.add_argument("--dtype", default="bf16", choices=["bf16", "f16", "f32"])
     ap.add_argument("--no-infer", action="store_true")
+    ap.add_argument("--loss", default="compute", choices=["compute", "surrogate"],
+                    help="compute: the reference's ComputeLoss semantics on the GPU (loss.py:94-677) with "
+                         "synthetic targets; surrogate: sum of mean(o^2) over the head maps")
+    ap.add_argument("--gts", type=int, default=8, help="synthetic ground-truth boxes per image (--loss compute)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--mode", default="both", choices=["both", "train", "infer"])
@@ -171,9 +175,22 @@ def _oracle(version):
     return M
 
 
-def cpu_baseline_train(version, nc, size, batch=8, steps=8):
-    """Oracle (fp32 torch-CPU restatement of the reference graph) train step on host cores."""
+def synth_targets(batch, nc, per_img, seed, device="cpu"):
+    """[batch*per_img, 6] collated targets (image, class, cx, cy, w, h normalised), boxes 5-45% of
+    the image side, fully inside it (the dataloader's format, dataset.py:235-267)."""
+    g = torch.Generator().manual_seed(seed)
+    n = batch * per_img
+    wh = torch.rand(n, 2, generator=g) * 0.4 + 0.05
+    c = torch.rand(n, 2, generator=g) * (1 - wh) + wh / 2
+    img = torch.arange(batch).repeat_interleave(per_img).float()
+    cls = torch.randint(0, nc, (n,), generator=g).float()
+    return torch.cat([img[:, None], cls[:, None], c, wh], 1).to(device)
+
+
+def cpu_baseline_train(version, nc, size, batch=8, steps=8, loss="compute", gts=8):
+    """Oracle (fp32 torch-CPU restatement of the reference graph and loss) train step on host cores."""
     M = _oracle(version)
+    from oracle import loss_ref
     threads = cpu_threads()
     sd = M.init_params(version, nc)
     p = {k: (t.clone().requires_grad_(True) if t.is_floating_point() and "running" not in k
@@ -181,11 +198,15 @@ def cpu_baseline_train(version, nc, size, batch=8, steps=8):
     params = [t for k, t in p.items() if t.requires_grad]
     opt = torch.optim.SGD(params, lr=0.01, momentum=0.937, nesterov=True, weight_decay=5e-4)
     x = torch.randn(batch, 3, size, size, generator=torch.Generator().manual_seed(0))
+    tg = synth_targets(batch, nc, gts, 0)
 
     def step():
         opt.zero_grad()
         outs = M.forward(p, version, nc, x, True)
-        sum((o ** 2).mean() for o in outs).backward()
+        if loss == "compute":
+            loss_ref.compute_loss(list(outs), tg, nc, (size, size))[0].backward()
+        else:
+            sum((o ** 2).mean() for o in outs).backward()
         opt.step()
 
     step()
@@ -194,7 +215,7 @@ def cpu_baseline_train(version, nc, size, batch=8, steps=8):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads,
-            "kind": "port", "sample": f"oracle/model_ref.py train step (fwd+bwd+SGD), fp32, B={batch}, "
+            "kind": "port", "sample": f"oracle/model_ref.py train step (fwd+{'loss_ref ComputeLoss' if loss == 'compute' else 'surrogate loss'}+bwd+SGD), fp32, B={batch}, "
             f"{size}x{size}, {steps} timed steps after 1 warmup ({dt:.1f} s), torch threads={threads} "
             f"(OMP_NUM_THREADS share of a host reporting {os.cpu_count()} cpus)"}
 
@@ -264,12 +285,19 @@ def main():
                               foreach=True)
         g = torch.Generator(device=dev).manual_seed(1234 + rank)
         x = torch.randn(a.batch, 3, a.size, a.size, device=dev, generator=g)
+        if a.loss == "compute":
+            from yolov8.tools.loss import ComputeLoss
+            crit = ComputeLoss(model.head, a.nc, dev, (a.size, a.size))
+            tg = synth_targets(a.batch, a.nc, a.gts, 4321 + rank, dev)
 
         def train_step():
             opt.zero_grad(set_to_none=True)
             outs = net(x)
-            # surrogate sum_i mean(o_i^2)
-            loss = sum(MeanSquare.apply(o) for o in outs)
+            if a.loss == "compute":
+                loss = crit.loss_tensor(outs, tg)[0]      # device tensor: no host sync in the step
+            else:
+                # surrogate sum_i mean(o_i^2)
+                loss = sum(MeanSquare.apply(o) for o in outs)
             loss.backward()
             opt.step()
 
@@ -346,8 +374,9 @@ def main():
                                           "allreduce+SGD-nesterov step",
                               "global_batch": a.batch * world, "per_gpu_batch": a.batch, "img": a.size,
                               "parallelism": f"dp{world}",
-                              "loss": "surrogate sum(mean(o^2)) over the 3 head maps (reference loss "
-                                      "crashes for nc=80, SURVEY 0.5)",
+                              "loss": (f"ComputeLoss semantics (tools/loss.py:94-677) on the GPU, {a.gts} synthetic "
+                                       "GT boxes per image" if a.loss == "compute" else
+                                       "surrogate sum(mean(o^2)) over the 3 head maps"),
                               "conv_gflop_per_img_fwd": round(flops_img / 1e9, 3),
                               "depthwise_gflop_per_img_fwd": round(dw_flops_img / 1e9, 3),
                               "peak_hbm_gib": round(tr["peak_gb"], 2),
@@ -377,7 +406,7 @@ def main():
         if world == 1 and not a.no_cpu_baseline:
             log("[rank 0] cpu baseline (oracle on host cores)...")
             if "train" in result:
-                line["cpu_baseline"] = cpu_baseline_train(a.version, a.nc, a.size)
+                line["cpu_baseline"] = cpu_baseline_train(a.version, a.nc, a.size, loss=a.loss, gts=a.gts)
             if "infer" in result:
                 cb = cpu_baseline_infer(a.version, a.nc, a.size)
                 if "cpu_baseline" in line:

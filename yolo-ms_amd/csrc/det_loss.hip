@@ -30,6 +30,7 @@ constexpr int DL_TOPK = 10;
 constexpr float DL_IOU_MIN = 0.1f;
 constexpr float DL_EPS = 1e-7f;
 constexpr int DL_MAXL = 4;
+constexpr int DL_ASSIGN_LDS = 4096;     // target rows staged per image in assign_kernel
 
 struct LossLevels {
   const void* x[DL_MAXL];   // head maps, NHWC with channel stride ld
@@ -215,10 +216,33 @@ __global__ __launch_bounds__(256) void assign_kernel(const float* tg, int M, int
   unsigned* bits = cbits + (long)b * A * nw;
   for (int a = tid; a < A; a += 256) f[a] = 0;
   for (long i = tid; i < (long)A * nw; i += 256) bits[i] = 0u;
+  // this image's target rows, in target order (one scan of the image column)
+  __shared__ int mine[DL_ASSIGN_LDS];
+  __shared__ int nmine;
+  if (tid == 0) nmine = 0;
   __syncthreads();
-  for (int j = 0; j < M; ++j) {
+  const bool staged = M <= DL_ASSIGN_LDS;
+  if (staged) {
+    for (int j0 = 0; j0 < M; j0 += 256) {
+      const int j = j0 + tid;
+      const bool hit = j < M && tg[(long)j * 6] >= 0.f && (int)tg[(long)j * 6] == b;
+      const unsigned long long bal = __ballot(hit);
+      __shared__ int wcnt[4];
+      if ((tid & 63) == 0) wcnt[tid >> 6] = __popcll(bal);
+      __syncthreads();
+      int base = nmine;
+      for (int q = 0; q < (tid >> 6); ++q) base += wcnt[q];
+      if (hit) mine[base + __popcll(bal & ((1ull << (tid & 63)) - 1ull))] = j;
+      __syncthreads();
+      if (tid == 0) nmine += (wcnt[0] + wcnt[1]) + (wcnt[2] + wcnt[3]);
+      __syncthreads();
+    }
+  }
+  const int nj = staged ? nmine : M;
+  for (int jj = 0; jj < nj; ++jj) {
+    const int j = staged ? mine[jj] : jj;
     const float* t = tg + (long)j * 6;
-    if (!(t[0] >= 0.f) || (int)t[0] != b) continue;    // block-uniform
+    if (!staged && (!(t[0] >= 0.f) || (int)t[0] != b)) continue;    // block-uniform
     const int k = kcnt[j];
     const int lab = (int)t[1];
     if (tid < k) {
@@ -248,10 +272,17 @@ __global__ __launch_bounds__(256) void assign_kernel(const float* tg, int M, int
   if (tid == 0) nfg[b] = (sc[0] + sc[1]) + (sc[2] + sc[3]);
 }
 
-__device__ __forceinline__ float bce_logits(float x, float t, float pw) {
-  // BCEWithLogits: (1 - t) x + (1 + (pw - 1) t) softplus(-x)
-  const float sp = fmaxf(-x, 0.f) + log1pf(expf(-fabsf(x)));
-  return (1.f - t) * x + (1.f + (pw - 1.f) * t) * sp;
+// BCEWithLogits value (1 - t) x + (1 + (pw - 1) t) softplus(-x) and its derivative
+// sigmoid(x) (1 + (pw - 1) t) - pw t, from one exponential and one logarithm
+__device__ __forceinline__ float bce_logits(float x, float t, float pw, float& dx) {
+  const float e = __expf(-fabsf(x));
+  const float r = __builtin_amdgcn_rcpf(1.f + e);
+  const float sig = x >= 0.f ? r : e * r;
+  const float lw = 1.f + (pw - 1.f) * t;
+  dx = sig * lw - pw * t;
+  // log(1 + e) by the hardware logarithm: absolute error ~1e-7 (also where e < eps and log1p
+  // would keep more relative digits of a ~1e-7 term), well inside the loss tolerance
+  return (1.f - t) * x + lw * (fmaxf(-x, 0.f) + __logf(1.f + e));
 }
 
 // block partial sums (fixed order) of one float per thread -> part[slot]
@@ -272,10 +303,10 @@ __global__ __launch_bounds__(256) void cls_kernel(LossLevels L, int A, int nc, i
                                                   float* part) {
   const int b = blockIdx.y;
   const int G = (nc + 7) / 8;
-  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  const int i = blockIdx.x * 256 + threadIdx.x;       // A * G < 2^31 (host-checked): 32-bit division
   float acc = 0.f;
-  if (i < (long)A * G) {
-    const int a = (int)(i / G), q = (int)(i - (long)a * G);
+  if (i < A * G) {
+    const int a = i / G, q = i - a * G;
     const int c0 = q * 8, nv = min(8, nc - c0);
     int l;
     float ax, ay;
@@ -292,9 +323,9 @@ __global__ __launch_bounds__(256) void cls_kernel(LossLevels L, int A, int nc, i
         const int c = c0 + k;
         const float t = (bits[c >> 5] >> (c & 31)) & 1u ? 1.f : 0.f;
         const float pw = pos_weight ? pos_weight[c] : 1.f;
-        acc += bce_logits(x[k], t, pw);
-        const float s = 1.f / (1.f + expf(-x[k]));
-        gr[k] = (s * (1.f + (pw - 1.f) * t) - pw * t) * f * gscale;
+        float dx;
+        acc += bce_logits(x[k], t, pw, dx);
+        gr[k] = dx * f * gscale;
       }
     }
     if (L.g[l]) store8(reinterpret_cast<T*>(L.g[l]) + row, nv, gr);
@@ -525,27 +556,36 @@ __global__ void flags_kernel(int B, int gx, const float* part, float* flags) {
   flags[2 * b + 1] = nd;
 }
 
-__global__ void finalize_kernel(int B, int A, int nc, int gxc, const float* pcls, int gxb, const float* pbox,
-                                const int* nfg, float lam_box, float lam_cls, float lam_dfl, float* out) {
+// per-image sums in fixed order (one thread per image), then thread 0 combines the images
+__global__ __launch_bounds__(256) void finalize_kernel(int B, int A, int nc, int gxc, const float* pcls, int gxb,
+                                                       const float* pbox, const int* nfg, float lam_box,
+                                                       float lam_cls, float lam_dfl, double* img, float* out) {
+  for (int b = threadIdx.x; b < B; b += blockDim.x) {
+    double s0 = 0.0, s1 = 0.0, s2 = 0.0, s3 = 0.0;
+    const float* pc = pcls + (long)b * gxc;
+    int k = 0;
+    for (; k + 3 < gxc; k += 4) { s0 += pc[k]; s1 += pc[k + 1]; s2 += pc[k + 2]; s3 += pc[k + 3]; }
+    for (; k < gxc; ++k) s0 += pc[k];
+    const double mean = ((s0 + s1) + (s2 + s3)) / ((double)A * (double)nc);
+    double cls = mean, box = 0.0, dfl = 0.0;
+    if (nfg[b] > 0) {
+      cls = 2.0 * mean;                                  // loss.py:530 + :551
+      double sb = 0.0, sd = 0.0, fb = 0.0, fd = 0.0;
+      for (int q = 0; q < gxb; ++q) {
+        const float* p = pbox + ((long)b * gxb + q) * 4;
+        sb += p[0]; sd += p[1]; fb += p[2]; fd += p[3];
+      }
+      if (fb == 0.0) box = sb / (double)nfg[b];
+      if (fd == 0.0) dfl = sd / (4.0 * (double)nfg[b]);
+    }
+    img[3 * b] = cls;
+    img[3 * b + 1] = box;
+    img[3 * b + 2] = dfl;
+  }
+  __syncthreads();
   if (threadIdx.x != 0) return;
   double lcls = 0.0, lbox = 0.0, ldfl = 0.0;
-  for (int b = 0; b < B; ++b) {
-    double s = 0.0;
-    for (int k = 0; k < gxc; ++k) s += (double)pcls[(long)b * gxc + k];
-    const double mean = s / ((double)A * (double)nc);
-    if (nfg[b] > 0) {
-      lcls += 2.0 * mean;
-      double sb = 0.0, sd = 0.0, fb = 0.0, fd = 0.0;
-      for (int k = 0; k < gxb; ++k) {
-        const float* q = pbox + ((long)b * gxb + k) * 4;
-        sb += q[0]; sd += q[1]; fb += q[2]; fd += q[3];
-      }
-      if (fb == 0.0) lbox += sb / (double)nfg[b];
-      if (fd == 0.0) ldfl += sd / (4.0 * (double)nfg[b]);
-    } else {
-      lcls += mean;
-    }
-  }
+  for (int b = 0; b < B; ++b) { lcls += img[3 * b]; lbox += img[3 * b + 1]; ldfl += img[3 * b + 2]; }
   lbox /= B; lcls /= B; ldfl /= B;
   out[0] = (float)(lam_box * lbox + lam_cls * lcls + lam_dfl * ldfl);
   out[1] = (float)lbox;
@@ -555,7 +595,7 @@ __global__ void finalize_kernel(int B, int A, int nc, int gxc, const float* pcls
 
 // workspace layout (bytes, 256-aligned pieces)
 struct LossWs {
-  size_t pbox, kcnt, kidx, fg, tbox, tltrb, cbits, nfg, pcls, pboxp, flags, total;
+  size_t pbox, kcnt, kidx, fg, tbox, tltrb, cbits, nfg, pcls, pboxp, flags, img, total;
 };
 static LossWs loss_ws(int B, int A, int nc, int M) {
   auto al = [](size_t x) { return (x + 255) / 256 * 256; };
@@ -574,6 +614,7 @@ static LossWs loss_ws(int B, int A, int nc, int M) {
   w.pcls = o; o += al((size_t)B * gxc * 4);
   w.pboxp = o; o += al((size_t)B * gxb * 16);
   w.flags = o; o += al((size_t)B * 8);
+  w.img = o; o += al((size_t)B * 24);
   w.total = o;
   return w;
 }
@@ -597,6 +638,9 @@ yms_status yms_det_loss(int dtype, int batch, int nc, int nlevels, const void* c
       !lambdas || n_targets < 0 || (n_targets > 0 && !targets) || iou_type < 0 || iou_type > 3)
     return YMS_ERR_INVALID;
   if (ld < 4 * DL_DFL + nc || ld % 8) return YMS_ERR_INVALID;
+  long a_total = 0;
+  for (int l = 0; l < nlevels; ++l) a_total += (long)hs[l] * ws_[l];
+  if (a_total * ((nc + 7) / 8) >= (1l << 31) - 256) return YMS_ERR_UNSUPPORTED;
   LossLevels L{};
   L.nl = nlevels;
   L.ld = ld;
@@ -626,6 +670,7 @@ yms_status yms_det_loss(int dtype, int batch, int nc, int nlevels, const void* c
   float* pcls = (float*)(base + w.pcls);
   float* pboxp = (float*)(base + w.pboxp);
   float* flags = (float*)(base + w.flags);
+  double* img = (double*)(base + w.img);
   const int nw = (nc + 31) / 32;
   const int gxc = cdiv((long)A * ((nc + 7) / 8), 256), gxb = cdiv(A, 256);
   hipStream_t st = (hipStream_t)stream;
@@ -645,8 +690,8 @@ yms_status yms_det_loss(int dtype, int batch, int nc, int nlevels, const void* c
   if (grads)                                                                                                   \
     hipLaunchKernelGGL(boxgrad_kernel<T>, dim3(gxb, batch), dim3(256), 0, st, L, A, fg, tbox, tltrb, iou_type,  \
                        flags, lambdas[0], lambdas[2], batch, nfg);                                             \
-  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(64), 0, st, batch, A, nc, gxc, pcls, gxb, pboxp, nfg,       \
-                     lambdas[0], lambdas[1], lambdas[2], out);
+  hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, batch, A, nc, gxc, pcls, gxb, pboxp, nfg,      \
+                     lambdas[0], lambdas[1], lambdas[2], img, out);
   switch (dtype) {
     case YMS_F32: { YMS_LOSS_CASE(float) break; }
     case YMS_BF16: { YMS_LOSS_CASE(bf16) break; }
