@@ -369,7 +369,8 @@ def main():
             tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L",
                     "ms-l": "configs[3]: YOLO-MS-L (MS-Block / HKS 3-5-7-9 depthwise graph)",
                     "ms-s": "YOLO-MS-S (MS-Block / HKS graph)"}.get(a.version, f"custom: YOLO-MS-{a.version.upper()}")
-            line["config"] = {"workload": f"{tcfg} (reference YOLOv8-'{a.version}' graph) "
+            graph = "" if a.version.startswith("ms-") else f" (reference YOLOv8-'{a.version}' graph)"
+            line["config"] = {"workload": f"{tcfg}{graph} "
                                           f"{a.size}x{a.size} {a.dtype} training, B={a.batch}/GPU, fwd+loss+bwd+"
                                           "allreduce+SGD-nesterov step",
                               "global_batch": a.batch * world, "per_gpu_batch": a.batch, "img": a.size,
