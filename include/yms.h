@@ -219,6 +219,17 @@ yms_status yms_map_accumulate(int n_det, const float* scores, const int* labels,
                               const uint8_t* tp, const uint8_t* kept, int n_classes, const int* n_gt,
                               double* ap, double* map);
 
+/* ---- input pipeline ------------------------------------------------------ */
+/* dataset.py:132-134 per-sample A.Resize(INTER_LINEAR) + A.Normalize(mean, std) + ToTensorV2 and
+ * collate_fn's torch.stack (:260), batched: images = device array of n
+ * { const uint8_t* src; int h, w, pitch, flags; } (HWC RGB uint8 rows of `pitch` bytes; flags bit 0
+ * horizontal flip, bit 1 vertical flip, applied before the resize); out = [n][3][out_h][out_w] of
+ * dtype (YMS_F32 / YMS_BF16 / YMS_F16), (v / 255 - mean[c]) / std[c] (mean, std: host float[3]).
+ * cv2 half-pixel bilinear coordinates with edge clamping; fp32 weights (cv2's 8-bit fixed-point
+ * rounding is not reproduced). */
+yms_status yms_resize_normalize(int dtype, int n, const void* images, int out_h, int out_w, const float* mean,
+                                const float* std, void* out, void* stream);
+
 /* ---- detection loss ------------------------------------------------------- */
 /* The reference's ComputeLoss (yolov8/tools/loss.py:94-677; python binding
  * yolov8.tools.loss.ComputeLoss mirrors its constructor and call) on the raw training head maps:
