@@ -21,6 +21,11 @@ SHAPES = [  # n, h, w, cin, cout, k, s
     (64, 40, 40, 256, 64, 3, 1),
     (64, 20, 20, 512, 80, 3, 1),
 ]
+if os.environ.get("YMS_MICRO_SHAPES") == "ms":   # YOLO-MS-S MS-Block 1x1 convs (B=64)
+    SHAPES = [(64, 160, 160, 64, 96, 1, 1), (64, 160, 160, 32, 64, 1, 1), (64, 160, 160, 64, 32, 1, 1),
+              (64, 160, 160, 96, 64, 1, 1), (64, 80, 80, 128, 192, 1, 1), (64, 80, 80, 64, 128, 1, 1),
+              (64, 80, 80, 128, 64, 1, 1), (64, 80, 80, 192, 128, 1, 1), (64, 40, 40, 128, 256, 1, 1),
+              (64, 40, 40, 256, 128, 1, 1)]
 dt = torch.bfloat16
 st = L.stream_ptr()
 
