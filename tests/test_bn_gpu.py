@@ -69,9 +69,11 @@ def test_bn_bwd_matches_fp64(npix, c, act):
         L.call("yms_bn_act_bwd_apply", L.F32, npix, c, zd.data_ptr(), c, 0, gyd.data_ptr(), c, 0, scd.data_ptr(),
                shd.data_ptr(), mi.data_ptr(), coef.data_ptr(), act, out.data_ptr(), c, 0, None, 0, 0, 0, st)
         torch.cuda.synchronize()
-        # rows the reduce wrote are exactly [0, rows): the NaN tail is untouched and nothing is NaN
+        # rows the reduce wrote lie in [0, rows): the NaN tail is untouched; the two-kernel reduce
+        # writes exactly yms_bn_bwd_rows rows (the fused one may write fewer: <= 32768 / c)
         assert torch.isnan(ws[rows:]).all()
-        assert torch.isfinite(ws[:rows]).all()
+        if not fused:
+            assert torch.isfinite(ws[:rows]).all()
         assert int(cnt[0]) == 0          # the fused finalize leaves its counter at zero
         assert rel(dgd, dg) < 1e-5, fused
         assert rel(dbd, db) < 1e-5, fused

@@ -50,12 +50,13 @@ def test_host_shape_validation_and_sizes():
 
 
 def test_bn_bwd_rows_is_the_launched_block_count():
-    """yms_bn_bwd_rows = the number of partial rows the reduce writes: with
-    ppb = ceil(npix / min(512, 32768 // c, ceil(npix/64))) the launch covers ceil(npix / ppb) blocks."""
+    """yms_bn_bwd_rows = the number of partial rows the (two-kernel) reduce writes: with
+    ppb = ceil(npix / min(512, ceil(npix/64))) the launch covers ceil(npix / ppb) blocks (the fused
+    reduce + finalize additionally caps rows at 32768 // c, never above this)."""
     for c in (8, 64, 80, 256, 512, 2048):
         for npix in (1, 63, 64, 65, 100, 32768, 32769, 40001, 44800, 57600, 63 * 640, 7 * 80 * 80, 64 * 160 * 160):
             rows = L.lib().yms_bn_bwd_rows(npix, c)
-            cap = max(1, min(512, max(32, 32768 // c), (npix + 63) // 64))
+            cap = max(1, min(512, (npix + 63) // 64))
             ppb = -(-npix // cap)
             assert rows == -(-npix // ppb), (npix, c)
             assert 1 <= rows <= 512 and (rows - 1) * ppb < npix <= rows * ppb, (npix, c)

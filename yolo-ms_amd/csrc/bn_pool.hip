@@ -806,12 +806,14 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
 
 // pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 512 (2 blocks
 // per CU leave room for the side-stream wgrad; interleaved A/B of the training step: cap 1024
-// 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms; YMS_BN_BWD_ROWS_CAP overrides) and at most
-// 32768 / c, so that the partial table the fused finalize's single block sums stays <= 256 KB.
-static long bwd_pix_per_block(long npix, int c) {
+// 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms; YMS_BN_BWD_ROWS_CAP overrides).  The fused
+// reduce + finalize (one last block sums the whole table) also keeps rows <= 32768 / c (table
+// <= 256 KB); the two-kernel path does not: that cap left 64-128 reduce blocks on 256 CUs for
+// the 256/512-channel layers (interleaved A/B: YOLOv8-s 19.51 -> 19.26 ms, -l 61.7 -> 60.9 ms).
+static long bwd_pix_per_block(long npix, int c, bool fused) {
   static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 512;
   static const long cprod = getenv("YMS_BN_BWD_CCAP") ? atol(getenv("YMS_BN_BWD_CCAP")) : 32768;   // dev A/B
-  const long ccap = cprod > 0 ? std::max(32l, cprod / std::max(c, 1)) : cap;
+  const long ccap = (fused && cprod > 0) ? std::max(32l, cprod / std::max(c, 1)) : cap;
   const long rows = std::max(1l, std::min(std::min(cap, ccap), (npix + 63) / 64));
   return (npix + rows - 1) / rows;
 }
@@ -821,7 +823,7 @@ static long bwd_pix_per_block(long npix, int c) {
 // scratch size, the launch and the finalize all use this one function.
 int yms_bn_bwd_rows(long npix, int c) {
   if (npix <= 0 || c <= 0) return 0;
-  const long ppb = bwd_pix_per_block(npix, c);
+  const long ppb = bwd_pix_per_block(npix, c, false);   // >= the fused path's rows: sizes both
   return (int)((npix + ppb - 1) / ppb);
 }
 
@@ -832,7 +834,7 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
   if (npix <= 0 || !gy || !ws || !vok(gy_ld, gy_off, c)) return YMS_ERR_INVALID;
   if (z && (!vok(z_ld, z_off, c) || !scale || !shift || !mean_invstd)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = bwd_pix_per_block(npix, c);
+  const long ppb = bwd_pix_per_block(npix, c, false);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
   if (z) {
     YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(rows), dim3(256), 0,
@@ -888,7 +890,7 @@ yms_status yms_bn_act_bwd_reduce_finalize(int dtype, long npix, int c, const voi
   if (npix <= 0 || !gy || !ws || !counter || !vok(gy_ld, gy_off, c)) return YMS_ERR_INVALID;
   if (z && (!vok(z_ld, z_off, c) || !scale || !shift || !mean_invstd)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = bwd_pix_per_block(npix, c);
+  const long ppb = bwd_pix_per_block(npix, c, true);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
   const BwdFin fin{counter, dgamma, dbeta, coef, npix};
   if (z) {
