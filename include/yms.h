@@ -54,6 +54,9 @@ typedef struct {
 } yms_conv_shape;
 
 const char* yms_version(void);
+/* A new stream restricted to ncus CUs (mode 0: lowest CU indices, 1: spread), for the backward's
+ * weight-gradient side stream (hipExtStreamCreateWithCUMask).  *stream_out: hipStream_t. */
+yms_status yms_stream_create_cu_subset(int ncus, int mode, void** stream_out);
 const char* yms_status_string(yms_status s);
 
 /* ---- weights ------------------------------------------------------------------------ */

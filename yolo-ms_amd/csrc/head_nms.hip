@@ -14,6 +14,8 @@
 //           ratio compared as double), FP contraction disabled, so keep indices are
 //           bit-exact against the CPU oracle on identical decoded inputs.
 #include <cstdlib>
+#include <vector>
+
 #include "yms_common.hpp"
 
 #pragma clang fp contract(off)
@@ -798,6 +800,27 @@ using namespace yms;
 extern "C" {
 
 const char* yms_version(void) { return "yms-mi355x 0.1 (gfx950)"; }
+
+// A stream whose kernels may only occupy `ncus` of the device's CUs (the backward's weight-gradient
+// side stream: the critical-path stream then always finds free CUs).  mode 0: the lowest CU
+// indices; mode 1: spread evenly over the index space.
+yms_status yms_stream_create_cu_subset(int ncus, int mode, void** stream_out) {
+  if (!stream_out || ncus <= 0) return YMS_ERR_INVALID;
+  int dev = 0, n = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+    return YMS_ERR_LAUNCH;
+  if (ncus > n) ncus = n;
+  std::vector<uint32_t> mask((n + 31) / 32, 0u);
+  for (int i = 0; i < ncus; ++i) {
+    const int cu = mode == 1 ? (int)((long)i * n / ncus) : i;
+    mask[cu >> 5] |= 1u << (cu & 31);
+  }
+  hipStream_t st = nullptr;
+  if (hipExtStreamCreateWithCUMask(&st, (uint32_t)mask.size(), mask.data()) != hipSuccess) return YMS_ERR_LAUNCH;
+  *stream_out = (void*)st;
+  return YMS_OK;
+}
 
 const char* yms_status_string(yms_status s) {
   switch (s) {

@@ -118,10 +118,23 @@ WGRAD_SIDE_STREAM = os.environ.get("YMS_WGRAD_STREAM", "1") != "0"
 _SIDE = {}
 
 
+# YMS_SIDE_CUS=k: the side stream may only use k CUs (YMS_SIDE_CU_MODE 0 lowest ids / 1 spread)
+SIDE_CUS = int(os.environ.get("YMS_SIDE_CUS", "0"))
+SIDE_CU_MODE = int(os.environ.get("YMS_SIDE_CU_MODE", "1"))
+
+
 def _side_stream(dev):
     s = _SIDE.get(dev)
     if s is None:
-        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
+        if SIDE_CUS > 0:
+            import ctypes
+            with torch.cuda.device(dev):
+                h = ctypes.c_void_p()
+                L.call("yms_stream_create_cu_subset", SIDE_CUS, SIDE_CU_MODE, ctypes.byref(h))
+                s = torch.cuda.ExternalStream(h.value, device=dev)
+        else:
+            s = torch.cuda.Stream(device=dev)
+        _SIDE[dev] = s
     return s
 
 
