@@ -1,0 +1,42 @@
+"""Dev tool: depthwise k x k kernels in isolation (B=64 YOLO-MS-S shapes): us and GB/s."""
+import ctypes, os, sys
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "yolo-ms_amd")]
+import torch
+from yms import _lib as L
+
+st = L.stream_ptr()
+for (n, h, w, c, k) in [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9),
+                        (64, 80, 80, 64, 3), (64, 40, 40, 128, 3)]:
+    sh = L.DwShape(n, h, w, c, k, L.BF16)
+    sp = ctypes.pointer(sh)
+    x = torch.randn(n, h, w, c, device="cuda").to(torch.bfloat16)
+    y = torch.empty_like(x)
+    wt = torch.randn(c, 1, k, k, device="cuda")
+    sc, sf = torch.ones(c, device="cuda"), torch.zeros(c, device="cuda")
+    rows = L.lib().yms_dwconv_stats_rows(sp)
+    stt = torch.empty(rows * (2 * c + 1), device="cuda")
+    wsb = L.lib().yms_dwconv_wgrad_ws_bytes(sp)
+    ws = torch.empty(wsb // 4 + 1, device="cuda")
+    dw = torch.empty(c, 1, k, k, device="cuda")
+    ops = {
+        "fwd": lambda: L.call("yms_dwconv_fwd", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0,
+                              sc.data_ptr(), sf.data_ptr(), 1, None, 0, st),
+        "fwd_stats": lambda: L.call("yms_dwconv_fwd", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0,
+                                    None, None, 0, stt.data_ptr(), c, st),
+        "dgrad": lambda: L.call("yms_dwconv_dgrad", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0, 0, st),
+        "wgrad": lambda: L.call("yms_dwconv_wgrad", sp, x.data_ptr(), c, 0, y.data_ptr(), c, 0, ws.data_ptr(), wsb,
+                                dw.data_ptr(), 0, st),
+    }
+    nb = x.numel() * 2 * 2
+    for name, fn in ops.items():
+        for _ in range(3):
+            fn()
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        for _ in range(10):
+            fn()
+        e.record()
+        torch.cuda.synchronize()
+        us = s.elapsed_time(e) * 100
+        print(f"{name:9s} {n}x{h}x{w} c{c} k{k}: {us:8.1f} us  {nb / us / 1e3:7.0f} GB/s", flush=True)

@@ -13,8 +13,9 @@
 // row and accumulates RX outputs in fp32 registers.
 //   forward: y = act(conv * scale + shift) (eval, BN folded) | z + per-tile BN partial sums (train)
 //   dgrad  : dx (+)= conv(dz, rot180(w))
-//   wgrad  : dw[c][t] = sum_p x[p + d_t][c] dz[p][c]: per-lane sliding partials, wave butterfly
-//            reduction per kernel row into an LDS accumulator, per-block rows + fixed-order reduce
+//   wgrad  : dw[c][t] = sum_p x[p + d_t][c] dz[p][c]: per-lane (kernel row, tile row, column
+//            segment) register partials across all of a block's tiles, one fixed-order LDS
+//            reduction per block, per-block rows + fixed-order reduce
 #include <algorithm>
 #include <cstdlib>
 
@@ -43,11 +44,11 @@ struct DwParams {
 };
 
 // stage the (TY + K - 1) x (TX + K - 1) halo of 32 channels (zero outside the image / past C)
-template <typename T, int K>
+template <typename T, int K, int NT = 256>
 __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, int n, int y0, int x0, int c0) {
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1, P = K / 2;
   const T* src = reinterpret_cast<const T*>(p.src);
-  for (int it = threadIdx.x; it < DW_G * HH * HW; it += 256) {
+  for (int it = threadIdx.x; it < DW_G * HH * HW; it += NT) {
     const int g = it / (HH * HW), r = it - g * (HH * HW);
     const int hy = r / HW, hx = r - hy * HW;
     const int y = y0 + hy - P, x = x0 + hx - P, c = c0 + 8 * g;
@@ -195,100 +196,129 @@ __global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
   }
 }
 
-// wgrad: blocks walk spatial tiles blockIdx.x, blockIdx.x + gridDim.x, ...; per tile the x halo and
-// the dz tile are staged; lane partials per kernel row are butterfly-reduced across the wave and
-// accumulated (fixed order) in LDS; the block writes ws[blockIdx.x][tap][c]
+// wgrad: a 512-thread block owns 32 channels (4 groups of 8, 128 lanes each) and walks the
+// spatial tiles blockIdx.x, blockIdx.x + gridDim.x, ...; per tile the x halo and the dz tile are
+// staged in LDS.  Lane (dy, ty, s) of a group owns kernel row dy, tile row ty and column segment s
+// (S segments of SL = 32 / S columns, K * 8 * S <= 128 lanes active) and keeps the K x 8 partial
+// taps dw[dy][0..K)[8 channels] in registers across ALL its tiles: per 4 columns it reads the 4 dz
+// values and the 4 + K - 1 halo values once and does 4 K 8 FMAs.  One fixed-order LDS reduction
+// over (ty, s) at the end writes ws[blockIdx.x][tap][c]; dwconv_wgrad_reduce_kernel sums the blocks.
+template <int K>
+struct DwWg {
+  static constexpr int S = K == 3 ? 4 : (K == 9 ? 1 : 2);
+  static constexpr int SL = DW_TX / S;
+  static constexpr int NA = K * DW_TY * S;   // active lanes per channel group
+};
+constexpr int DW_WG_NT = 512, DW_WG_LPG = DW_WG_NT / DW_G;
+
 template <typename T, int K>
-__global__ __launch_bounds__(256) void dwconv_wgrad_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
-                                                           float* ws) {
+__global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
+                                                                 float* ws) {
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1;
-  __shared__ Raw8<T> halo[DW_G * HH * HW];
-  __shared__ float accw[DW_G][K * K][8];
+  constexpr int S = DwWg<K>::S, SL = DwWg<K>::SL, NA = DwWg<K>::NA;
+  static_assert(NA <= DW_WG_LPG && SL % 4 == 0, "dw wgrad lane mapping");
+  constexpr int HALO = DW_G * HH * HW, DZN = DW_G * DW_TY * DW_TX;
+  constexpr int STAGE_B = (HALO + DZN) * (int)sizeof(Raw8<T>);
+  constexpr int RED_B = NA * K * 8 * (int)sizeof(float);
+  __shared__ __attribute__((aligned(16))) char smem[STAGE_B > RED_B ? STAGE_B : RED_B];
+  Raw8<T>* halo = reinterpret_cast<Raw8<T>*>(smem);
+  Raw8<T>* dzl = halo + HALO;
+  float* red = reinterpret_cast<float*>(smem);
   const int c0 = blockIdx.y * DW_CB;
-  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ty = lane >> 3, qx = lane & 7;
-  for (int it = threadIdx.x; it < DW_G * K * K * 8; it += 256) (&accw[0][0][0])[it] = 0.0f;
+  const int g = threadIdx.x / DW_WG_LPG, l = threadIdx.x % DW_WG_LPG;
+  const bool active = l < NA;
+  const int ll = active ? l : 0;
+  const int dy = ll / (DW_TY * S), r = ll % (DW_TY * S);
+  const int ty = r / S, sx = (r % S) * SL;
+  float part[K][8];
+#pragma unroll
+  for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[dx][k] = 0.0f;
   const int per_img = p.tiles_x * p.tiles_y, ntiles = p.N * per_img;
-  const int c = c0 + 8 * g, nv = min(8, p.C - c);
   const T* dzp = reinterpret_cast<const T*>(dz);
   for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
     const int n = tile / per_img, rem = tile - n * per_img;
     const int y0 = (rem / p.tiles_x) * DW_TY, x0 = (rem % p.tiles_x) * DW_TX;
-    __syncthreads();      // previous tile's halo reads are done
-    dw_stage_halo<T, K>(p, halo, n, y0, x0, c0);
-    // the lane's RX dz values (zero outside the image / past C)
-    float d[DW_RX][8];
-    const int y = y0 + ty;
+    __syncthreads();      // previous tile's LDS reads are done
+    dw_stage_halo<T, K, DW_WG_NT>(p, halo, n, y0, x0, c0);
+    for (int it = threadIdx.x; it < DZN; it += DW_WG_NT) {
+      const int g2 = it / (DW_TY * DW_TX), r2 = it - g2 * (DW_TY * DW_TX);
+      const int y = y0 + r2 / DW_TX, x = x0 + r2 % DW_TX, c = c0 + 8 * g2;
+      Raw8<T> v;
 #pragma unroll
-    for (int i = 0; i < DW_RX; ++i) {
-      const int x = x0 + 4 * qx + i;
-      if (nv > 0 && y < p.H && x < p.W) {
-        load8(dzp + (((long)n * p.H + y) * p.W + x) * dz_ld + dz_off + c, nv, d[i]);
-      } else {
-#pragma unroll
-        for (int k = 0; k < 8; ++k) d[i][k] = 0.0f;
-      }
+      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) v.v[k] = u32x4{0u, 0u, 0u, 0u};
+      if (y < p.H && x < p.W && c < p.C)
+        load_raw8(dzp + (((long)n * p.H + y) * p.W + x) * dz_ld + dz_off + c, min(8, p.C - c), v);
+      dzl[it] = v;
     }
     __syncthreads();
-    const Raw8<T>* hp = halo + g * HH * HW;
-#pragma unroll 1
-    for (int dy = 0; dy < K; ++dy) {
-      float part[K][8];
+    if (active) {
+      const Raw8<T>* hrow = halo + g * HH * HW + (ty + dy) * HW + sx;
+      const Raw8<T>* drow = dzl + g * DW_TY * DW_TX + ty * DW_TX + sx;
+#pragma unroll 2
+      for (int x4 = 0; x4 < SL; x4 += 4) {
+        float d[4][8];
 #pragma unroll
-      for (int dx = 0; dx < K; ++dx)
+        for (int i = 0; i < 4; ++i) unpack8(drow[x4 + i], d[i]);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) part[dx][k] = 0.0f;
-      const Raw8<T>* row = hp + (ty + dy) * HW + 4 * qx;
+        for (int q = 0; q < 4 + K - 1; ++q) {
+          float v[8];
+          unpack8(hrow[x4 + q], v);
 #pragma unroll
-      for (int q = 0; q < DW_RX + K - 1; ++q) {
-        float v[8];
-        unpack8(row[q], v);
+          for (int i = 0; i < 4; ++i) {
+            const int dx = q - i;
+            if (dx >= 0 && dx < K) {
 #pragma unroll
-        for (int i = 0; i < DW_RX; ++i) {
-          const int dx = q - i;
-          if (dx >= 0 && dx < K) {
-#pragma unroll
-            for (int k = 0; k < 8; ++k) part[dx][k] += v[k] * d[i][k];
+              for (int k = 0; k < 8; ++k) part[dx][k] += v[k] * d[i][k];
+            }
           }
         }
       }
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx)
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float v = part[dx][k];
-#pragma unroll
-          for (int m = 1; m < 64; m <<= 1) v += __shfl_xor(v, m);
-          part[dx][k] = v;
-        }
-      // lane (dx * 8 + k) < K * 8 adds tap (dy, dx) channel k -- one writer per element
-#pragma unroll
-      for (int dx = 0; dx < K; ++dx)
-#pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (lane == ((dx * 8 + k) & 63)) accw[g][dy * K + dx][k] += part[dx][k];
     }
   }
-  __syncthreads();
-  float* out = ws + (long)blockIdx.x * K * K * p.C;
-  for (int it = threadIdx.x; it < DW_G * K * K * 8; it += 256) {
-    const int gg = it / (K * K * 8), r = it - gg * (K * K * 8);
-    const int t = r / 8, k = r - t * 8;
-    const int cc = c0 + 8 * gg + k;
-    if (cc < p.C) out[(long)t * p.C + cc] = accw[gg][t][k];
+  // fixed-order reduction over the (ty, s) lanes of each kernel row, one channel group at a time
+  for (int gg = 0; gg < DW_G; ++gg) {
+    __syncthreads();
+    if (g == gg && active) {
+      float* rp = red + l * K * 8;
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        *reinterpret_cast<f32x4*>(rp + dx * 8) = f32x4{part[dx][0], part[dx][1], part[dx][2], part[dx][3]};
+        *reinterpret_cast<f32x4*>(rp + dx * 8 + 4) = f32x4{part[dx][4], part[dx][5], part[dx][6], part[dx][7]};
+      }
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < K * K * 8; it += DW_WG_NT) {
+      const int t = it / 8, k = it - t * 8;
+      const int ddy = t / K, ddx = t - ddy * K;
+      float s = 0.f;
+      for (int rr = 0; rr < DW_TY * S; ++rr) s += red[((ddy * DW_TY * S + rr) * K + ddx) * 8 + k];
+      const int cc = c0 + 8 * gg + k;
+      if (cc < p.C) ws[((long)blockIdx.x * K * K + t) * p.C + cc] = s;
+    }
   }
 }
 
-// dw[c][t] (+)= sum_b ws[b][t][c], fixed order over b
+// dw[c][t] (+)= sum_b ws[b][t][c]: 64 outputs per block, wave w sums blocks b = w (mod 4) in order,
+// the four partials are added in a fixed order
 __global__ __launch_bounds__(256) void dwconv_wgrad_reduce_kernel(const float* ws, int blocks, int C, int KK, float* dw,
                                                                   int accumulate) {
-  const int idx = blockIdx.x * 256 + threadIdx.x;
-  if (idx >= C * KK) return;
-  const int t = idx / C, c = idx - t * C;
+  __shared__ float red[4][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int j = blockIdx.x * 64 + lane;
+  const long stride = (long)C * KK;
   float s = 0.f;
-  for (int b = 0; b < blocks; ++b) s += ws[((long)b * KK + t) * C + c];
-  float* o = dw + (long)c * KK + t;
-  *o = accumulate ? *o + s : s;
+  if (j < stride)
+    for (int b = w; b < blocks; b += 4) s += ws[(long)b * stride + j];
+  red[w][lane] = s;
+  __syncthreads();
+  if (w == 0 && j < stride) {
+    s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const int t = j / C, c = j - t * C;
+    float* o = dw + (long)c * KK + t;
+    *o = accumulate ? *o + s : s;
+  }
 }
 
 static int dw_tiles(const yms_dw_shape* s, int& tx, int& ty) {
@@ -303,10 +333,13 @@ static bool dw_shape_ok(const yms_dw_shape* s) {
 }
 static bool dw_view_ok(int ld, int off, int c) { return ld % 8 == 0 && off % 8 == 0 && off + c <= ld; }
 
+// spatial partitions of the wgrad grid: about 1024 blocks in total over the channel groups (two
+// 512-thread blocks fit a CU), each walking several tiles so the ws rows stay few
 static int dw_wgrad_blocks(const yms_dw_shape* s) {
   int tx, ty;
   const int t = dw_tiles(s, tx, ty);
-  return std::max(1, std::min(t, 1024));
+  const int cg = (s->c + DW_CB - 1) / DW_CB;
+  return std::max(1, std::min(t, std::max(1, 1024 / cg)));
 }
 
 #define YMS_DW_K(K, ...)                                        \
@@ -408,12 +441,12 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
   const int blocks = dw_wgrad_blocks(s);
   dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
   hipStream_t st = (hipStream_t)stream;
-  YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK>), grid, dim3(256), 0, st, p,
+  YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK>), grid, dim3(DW_WG_NT), 0, st, p,
                                                       (const char*)dz, dz_ld, dz_off, ws)));
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
   const int KK2 = s->k * s->k;
-  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 255) / 256)), dim3(256), 0, st, ws,
+  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(256), 0, st, ws,
                      blocks, s->c, KK2, dw, accumulate);
   return launch_status();
 }
