@@ -6,8 +6,13 @@ import torch
 from yms import _lib as L
 
 st = L.stream_ptr()
-for (n, h, w, c, k) in [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9),
-                        (64, 80, 80, 64, 3), (64, 40, 40, 128, 3)]:
+SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9),
+          (64, 80, 80, 64, 3), (64, 40, 40, 128, 3)]
+if os.environ.get("YMS_MICRO_SHAPES") == "k9":
+    SHAPES = [(64, 20, 20, 512, 9)]
+if os.environ.get("YMS_MICRO_SHAPES") == "mss":   # YOLO-MS-S depthwise layers at B=64
+    SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 384, 3), (64, 40, 40, 768, 3), (64, 20, 20, 512, 3)]
+for (n, h, w, c, k) in SHAPES:
     sh = L.DwShape(n, h, w, c, k, L.BF16)
     sp = ctypes.pointer(sh)
     x = torch.randn(n, h, w, c, device="cuda").to(torch.bfloat16)
@@ -20,6 +25,9 @@ for (n, h, w, c, k) in [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40
     ws = torch.empty(wsb // 4 + 1, device="cuda")
     dw = torch.empty(c, 1, k, k, device="cuda")
     ops = {
+        "dgrad0": lambda: L.call("yms_dwconv_dgrad", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0, 0, st),
+        "fwd_noact": lambda: L.call("yms_dwconv_fwd", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0,
+                                    None, None, 0, None, 0, st),
         "fwd": lambda: L.call("yms_dwconv_fwd", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0,
                               sc.data_ptr(), sf.data_ptr(), 1, None, 0, st),
         "fwd_stats": lambda: L.call("yms_dwconv_fwd", sp, x.data_ptr(), c, 0, wt.data_ptr(), y.data_ptr(), c, 0,

@@ -34,6 +34,10 @@ def call(name, *args):
         sh = args[0].contents
         key = f"{sh.n}x{sh.h}x{sh.w} {sh.cin}->{sh.cout} k{sh.k}s{sh.stride}"
         fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
+    elif name.startswith("yms_dwconv"):
+        sh = args[0].contents
+        key = f"{sh.n}x{sh.h}x{sh.w} c{sh.c} k{sh.k}"
+        fl = 2 * sh.n * sh.h * sh.w * sh.c * sh.k * sh.k
     elif name.startswith(("yms_bn_act", "yms_affine")):
         key = f"npix {args[1]} c {args[2]}"
         fl = 0

@@ -7,10 +7,10 @@
 //
 // Mapping: a 256-thread block owns a TY x TX = 8 x 32 output tile of one image and 32 channels;
 // wave w owns 8 channels (one 16-B NHWC chunk), lane (ty, qx) = (lane / 8, lane % 8) owns the
-// RX = 4 consecutive pixels (ty, 4 qx .. 4 qx + 3).  The (8 + k - 1) x (32 + k - 1) input halo of
-// the block's channels is staged once in LDS (planar per wave, zero outside the image) with the
-// block's k x k x 32 weights; per kernel row a lane slides an (RX + k - 1)-pixel window over its
-// row and accumulates RX outputs in fp32 registers.
+// RX = 4 consecutive pixels (ty, 4 qx .. 4 qx + 3).  Forward and dgrad blocks walk a vertical
+// strip of such tiles; the input rows (32 + k - 1 wide, zero outside the image) live in an LDS
+// ring, and the rows of the next tile are loaded while the current one computes.  Per kernel row a
+// lane slides an (RX + k - 1)-pixel window over its row and accumulates RX outputs in fp32.
 //   forward: y = act(conv * scale + shift) (eval, BN folded) | z + per-tile BN partial sums (train)
 //   dgrad  : dx (+)= conv(dz, rot180(w))
 //   wgrad  : dw[c][t] = sum_p x[p + d_t][c] dz[p][c]: per-lane (kernel row, tile row, column
@@ -19,7 +19,7 @@
 #include <algorithm>
 #include <cstdlib>
 
-#include "yms_common.hpp"
+#include "conv_common.hpp"
 
 namespace yms {
 
@@ -41,6 +41,7 @@ struct DwParams {
   int accumulate;
   int N, H, W, C;
   int tiles_x, tiles_y;  // spatial tiles per image
+  int ysplit, tps;       // forward / dgrad: strips per image column of tiles, tiles per strip
 };
 
 // stage the (TY + K - 1) x (TX + K - 1) halo of 32 channels (zero outside the image / past C)
@@ -61,138 +62,229 @@ __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, i
   }
 }
 
-template <typename T, int K, int MODE>
-__global__ __launch_bounds__(256) void dwconv_kernel(DwParams p) {
-  constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1;
-  __shared__ Raw8<T> halo[DW_G * HH * HW];
-  __shared__ __attribute__((aligned(16))) float wl[DW_G][K * K][8];
-  const int tile = blockIdx.x;
-  const int per_img = p.tiles_x * p.tiles_y;
-  const int n = tile / per_img, rem = tile - n * per_img;
-  const int y0 = (rem / p.tiles_x) * DW_TY, x0 = (rem % p.tiles_x) * DW_TX;
-  const int c0 = blockIdx.y * DW_CB;
-  dw_stage_halo<T, K>(p, halo, n, y0, x0, c0);
-  for (int it = threadIdx.x; it < DW_G * K * K * 8; it += 256) {
-    const int g = it / (K * K * 8), r = it - g * (K * K * 8);
-    const int t = r / 8, i = r - t * 8;
-    const int c = c0 + 8 * g + i;
-    // dgrad correlates with the kernel rotated by 180 degrees
-    const int tw = MODE == DW_DGRAD ? K * K - 1 - t : t;
-    wl[g][t][i] = c < p.C ? p.w[(long)c * K * K + tw] : 0.0f;
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+// one input row (image row y, halo columns x0 - P .. x0 + TX - 1 + P, the wave's 8 channels c) into
+// an LDS ring row (wave-uniform LDS byte address lds_row) by LDS-DMA, 16 B per lane, no registers;
+// out-of-image columns / rows and channels past C read as zeros through the buffer range check.
+// Inline asm on purpose: hipcc treats its own LDS-DMA as a pending write to the whole LDS object
+// and waits vmcnt(0) before the next ds_read, which would serialise this prefetch with the FMAs of
+// the current tile (the ring slots written and read are disjoint by construction); completion is
+// counted by hand (wait_vmcnt<0> + barrier at the end of each tile).  M0 is saved and restored in
+// the same statement (it is compiler-reserved).
+template <typename T, int K>
+__device__ __forceinline__ void dw_row_dma(i32x4 rs, uint32_t lds_row, int y, int x0, int c, int H, int W, int C,
+                                           int ld, int lane) {
+  constexpr int CPE = (int)sizeof(T) / 2, NCH = (DW_TX + K - 1) * CPE;
+#pragma unroll
+  for (int j0 = 0; j0 < NCH; j0 += 64) {
+    const int j = j0 + lane;
+    if (j < NCH) {
+      const int hx = j / CPE, part = j - hx * CPE;
+      const int x = x0 + hx - K / 2;
+      uint32_t vo = NT_OOB;
+      if (y >= 0 && y < H && x >= 0 && x < W && c < C)
+        vo = ((uint32_t)(y * W + x) * (uint32_t)ld + (uint32_t)c) * (uint32_t)sizeof(T) + 16u * part;
+      unsigned keep;
+      asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tbuffer_load_dwordx4 %1, %2, 0 offen lds\n\t"
+                   "s_mov_b32 m0, %0"
+                   : "=&s"(keep)
+                   : "v"(vo), "s"(rs), "s"(lds_row + 16u * j0)
+                   : "memory");
+    }
   }
-  __syncthreads();
+}
+
+// forward / dgrad: a block walks a vertical strip of tiles (p.tps tiles of one image column tile
+// and 32 channels), keeping the input rows in an LDS ring of RB = 2 TY + K - 1 rows: tile t reads
+// rows y0 - P .. y0 + TY - 1 + P while the TY rows the next tile adds stream into the other ring
+// slots by LDS-DMA (issued before the tile's FMAs, waited for at the tile's end), so each input
+// row crosses HBM once per strip and the loads overlap the arithmetic.  Row y lives in ring slot
+// (y + P) % RB; wave g loads the rows of its own channel group.
+// blocks per CU the forward / dgrad registers are budgeted for (LDS ring: 40 / 49 / 60 / 72 KB bf16)
+// (fp32 rings are twice as large: 1-2 blocks)
+template <typename T, int K> struct DwOcc {
+  static constexpr int v = sizeof(T) == 4 ? (K == 3 ? 2 : 1) : (K == 3 ? 4 : (K == 5 ? 3 : 2));
+};
+
+template <typename T, int K, int MODE>
+__global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams p) {
+  constexpr int P = K / 2, HW = DW_TX + K - 1, RB = 2 * DW_TY + K - 1;
+  // ONE __shared__ object: a second one beside the LDS-DMA target makes hipcc wait vmcnt(0) before
+  // the first ds_read of every kernel row (cdna_hip_programming.md, .s-level trap (a))
+  constexpr int RING_B = DW_G * RB * HW * (int)sizeof(Raw8<T>);
+  constexpr int WL_B = DW_G * K * K * 8 * (int)sizeof(float);
+  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + DW_G * 16 * (int)sizeof(float)];
+  Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
+  float (*wl)[K * K][8] = reinterpret_cast<float (*)[K * K][8]>(smem + RING_B);
+  float (*scl)[16] = reinterpret_cast<float (*)[16]>(smem + RING_B + WL_B);   // eval scale | shift (LDS:
+                                                                                // not live across the FMAs)
+  const int per_img = p.tiles_x * p.ysplit;
+  const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
+  const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
+  const int x0 = tx * DW_TX;
+  const int c0 = blockIdx.y * DW_CB;
+  {
+    // the block's 32 x K x K weights are one contiguous range of p.w: coalesced loads, all issued
+    // before the LDS stores (dgrad correlates with the kernel rotated by 180 degrees)
+    constexpr int NWL = (DW_CB * K * K + 255) / 256;
+    const int nvalid = min(DW_CB, p.C - c0) * K * K;
+    float wv[NWL];
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+      const int it = threadIdx.x + 256 * j;
+      wv[j] = it < nvalid ? p.w[(long)c0 * K * K + it] : 0.0f;
+    }
+#pragma unroll
+    for (int j = 0; j < NWL; ++j) {
+      const int it = threadIdx.x + 256 * j;
+      if (it < DW_CB * K * K) {
+        const int cl = it / (K * K), t = it - cl * (K * K);
+        const int tw = MODE == DW_DGRAD ? K * K - 1 - t : t;
+        wl[cl >> 3][tw][cl & 7] = wv[j];
+      }
+    }
+  }
+  if (MODE == DW_FWD_AFFINE && threadIdx.x < DW_G * 16) {
+    const int gg = threadIdx.x >> 4, k = threadIdx.x & 7, c = c0 + 8 * gg + k;
+    scl[gg][threadIdx.x & 15] = (threadIdx.x & 8) ? ((p.shift && c < p.C) ? p.shift[c] : 0.0f)
+                                                  : ((p.scale && c < p.C) ? p.scale[c] : 1.0f);
+  }
   const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ty = lane >> 3, qx = lane & 7;
-  const Raw8<T>* hp = halo + g * HH * HW;
-  float acc[DW_RX][8];
-#pragma unroll
-  for (int i = 0; i < DW_RX; ++i)
-#pragma unroll
-    for (int c = 0; c < 8; ++c) acc[i][c] = 0.0f;
-  // one kernel row at a time (not unrolled): the row's k x 8 weights live in registers
-#pragma unroll 1
-  for (int dy = 0; dy < K; ++dy) {
-    float wr[K][8];
-#pragma unroll
-    for (int dx = 0; dx < K; ++dx) {
-      const f32x4 a = *reinterpret_cast<const f32x4*>(&wl[g][dy * K + dx][0]);
-      const f32x4 b = *reinterpret_cast<const f32x4*>(&wl[g][dy * K + dx][4]);
-#pragma unroll
-      for (int c = 0; c < 4; ++c) { wr[dx][c] = a[c]; wr[dx][4 + c] = b[c]; }
+  const int c = c0 + 8 * g, nv = min(8, p.C - c);
+  // raw buffer resource over image n's rows (32-bit offsets: checked on the host)
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
+                                                   (long)n * p.H * p.W * p.src_ld + p.src_off);
+  const i32x4 rs = {(int)(uint32_t)ib, (int)(uint32_t)(ib >> 32) & 0xffff,
+                    (int)((long)p.H * p.W * p.src_ld * (long)sizeof(T)), NT_RSRC3};
+  const uint32_t myring = __builtin_amdgcn_readfirstlane(
+      (uint32_t)reinterpret_cast<uintptr_t>(ring + g * RB * HW));   // LDS byte address (wave-uniform)
+  constexpr uint32_t ROWB = HW * (uint32_t)sizeof(Raw8<T>);
+  // prologue: the first tile's TY + K - 1 rows
+  for (int hy = 0; hy < DW_TY + K - 1; ++hy)
+    dw_row_dma<T, K>(rs, myring + ((t0 * DW_TY + hy) % RB) * ROWB, t0 * DW_TY - P + hy, x0, c, p.H, p.W, p.C,
+                     p.src_ld, lane);
+  wait_vmcnt<0>();
+  __syncthreads();
+  for (int t = t0; t < t1; ++t) {
+    const int y0 = t * DW_TY;
+    const bool more = t + 1 < t1;
+    // the next tile's TY new rows y0 + TY + P .. y0 + 2 TY - 1 + P go to slots this tile does not read
+    if (more) {
+      int sl = (y0 + DW_TY + 2 * P) % RB;
+      for (int hy = 0; hy < DW_TY; ++hy) {
+        dw_row_dma<T, K>(rs, myring + sl * ROWB, y0 + DW_TY + P + hy, x0, c, p.H, p.W, p.C, p.src_ld, lane);
+        sl = sl + 1 == RB ? 0 : sl + 1;
+      }
     }
-    const Raw8<T>* row = hp + (ty + dy) * HW + 4 * qx;
+    const Raw8<T>* hp = ring + g * RB * HW + 4 * qx;
+    float acc[DW_RX][8];
 #pragma unroll
-    for (int q = 0; q < DW_RX + K - 1; ++q) {
-      float v[8];
-      unpack8(row[q], v);
+    for (int i = 0; i < DW_RX; ++i)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) acc[i][k] = 0.0f;
+    // one kernel row at a time (not unrolled): the row's k x 8 weights live in registers
+    int slot = (y0 + ty) % RB;   // ring slot of input row y0 + ty - P
+#pragma unroll 1
+    for (int dy = 0; dy < K; ++dy) {
+      float wr[K][8];
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        const f32x4 a = *reinterpret_cast<const f32x4*>(&wl[g][dy * K + dx][0]);
+        const f32x4 b = *reinterpret_cast<const f32x4*>(&wl[g][dy * K + dx][4]);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) { wr[dx][k] = a[k]; wr[dx][4 + k] = b[k]; }
+      }
+      const Raw8<T>* row = hp + slot * HW;
+#pragma unroll
+      for (int q = 0; q < DW_RX + K - 1; ++q) {
+        float v[8];
+        unpack8(row[q], v);
+#pragma unroll
+        for (int i = 0; i < DW_RX; ++i) {
+          const int dx = q - i;
+          if (dx >= 0 && dx < K) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) acc[i][k] += v[k] * wr[dx][k];
+          }
+        }
+      }
+      slot = slot + 1 == RB ? 0 : slot + 1;
+    }
+    const int tile = (n * p.tiles_y + t) * p.tiles_x + tx;   // statistics row (image-major tiles)
+    const int y = y0 + ty;
+    if (nv > 0 && y < p.H) {
+      T* dst = reinterpret_cast<T*>(p.dst);
 #pragma unroll
       for (int i = 0; i < DW_RX; ++i) {
-        const int dx = q - i;
-        if (dx >= 0 && dx < K) {
+        const int x = x0 + 4 * qx + i;
+        if (x >= p.W) continue;
+        float o[8];
 #pragma unroll
-          for (int c = 0; c < 8; ++c) acc[i][c] += v[c] * wr[dx][c];
+        for (int k = 0; k < 8; ++k) {
+          float v = acc[i][k];
+          if (MODE == DW_FWD_AFFINE) {
+            v = v * scl[g][k] + scl[g][8 + k];
+            if (p.act == YMS_ACT_SILU) v = silu_f(v);
+          }
+          o[k] = v;
         }
+        T* d = dst + (((long)n * p.H + y) * p.W + x) * p.dst_ld + p.dst_off + c;
+        if (MODE == DW_DGRAD && p.accumulate) {
+          float r[8];
+          load8(d, nv, r);
+#pragma unroll
+          for (int k = 0; k < 8; ++k) o[k] += r[k];
+        }
+        store8(d, nv, o);
       }
     }
-  }
-  const int c = c0 + 8 * g, nv = min(8, p.C - c);
-  const int y = y0 + ty;
-  float sc[8], sh[8];
-  if (MODE == DW_FWD_AFFINE) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      sc[k] = (p.scale && c + k < p.C) ? p.scale[c + k] : 1.0f;
-      sh[k] = (p.shift && c + k < p.C) ? p.shift[c + k] : 0.0f;
-    }
-  }
-  if (nv > 0 && y < p.H) {
-    T* dst = reinterpret_cast<T*>(p.dst);
-#pragma unroll
-    for (int i = 0; i < DW_RX; ++i) {
-      const int x = x0 + 4 * qx + i;
-      if (x >= p.W) continue;
-      float o[8];
+    if (MODE == DW_FWD_STATS) {
+      // one statistics row per spatial tile (conv_common.hpp contract; its pixel count goes to the
+      // count table after the rows): sum and centred M2 over the tile's valid pixels, two passes
+      // over the fp32 accumulators, wave butterflies in a fixed order
+      const int vy = min(DW_TY, p.H - y0), vx = min(DW_TX, p.W - x0);
+      const float inv_n = 1.0f / (float)(vy * vx);
+      float s1[8], m2[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        float v = acc[i][k];
-        if (MODE == DW_FWD_AFFINE) {
-          v = v * sc[k] + sh[k];
-          if (p.act == YMS_ACT_SILU) v = silu_f(v);
+        float s = 0.f;
+        if (y < p.H) {
+#pragma unroll
+          for (int i = 0; i < DW_RX; ++i)
+            if (x0 + 4 * qx + i < p.W) s += acc[i][k];
         }
-        o[k] = v;
-      }
-      T* d = dst + (((long)n * p.H + y) * p.W + x) * p.dst_ld + p.dst_off + c;
-      if (MODE == DW_DGRAD && p.accumulate) {
-        float r[8];
-        load8(d, nv, r);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) o[k] += r[k];
+        for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
+        const float mu = s * inv_n;
+        float q = 0.f;
+        if (y < p.H) {
+#pragma unroll
+          for (int i = 0; i < DW_RX; ++i)
+            if (x0 + 4 * qx + i < p.W) {
+              const float d = acc[i][k] - mu;
+              q += d * d;
+            }
+        }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) q += __shfl_xor(q, m);
+        s1[k] = s;
+        m2[k] = q;
       }
-      store8(d, nv, o);
+      if (lane < 8 && c + lane < p.C) {
+        float a = 0.f, b = 0.f;
+#pragma unroll
+        for (int k = 0; k < 8; ++k)
+          if (k == lane) { a = s1[k]; b = m2[k]; }
+        float* so = p.stats + (long)tile * 2 * p.stats_ld;
+        so[c + lane] = a;
+        so[p.stats_ld + c + lane] = b;
+      }
+      if (blockIdx.y == 0 && threadIdx.x == 0) p.stats_cnt[tile] = (float)(vy * vx);
     }
-  }
-  if (MODE == DW_FWD_STATS) {
-    // one statistics row per spatial tile (conv_common.hpp contract; its pixel count goes to the
-    // count table after the rows): sum and centred M2 over the tile's valid pixels, two passes
-    // over the fp32 accumulators, wave butterflies in a fixed order
-    const int vy = min(DW_TY, p.H - y0), vx = min(DW_TX, p.W - x0);
-    const float inv_n = 1.0f / (float)(vy * vx);
-    float s1[8], m2[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float s = 0.f;
-      if (y < p.H) {
-#pragma unroll
-        for (int i = 0; i < DW_RX; ++i)
-          if (x0 + 4 * qx + i < p.W) s += acc[i][k];
-      }
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
-      const float mu = s * inv_n;
-      float q = 0.f;
-      if (y < p.H) {
-#pragma unroll
-        for (int i = 0; i < DW_RX; ++i)
-          if (x0 + 4 * qx + i < p.W) {
-            const float d = acc[i][k] - mu;
-            q += d * d;
-          }
-      }
-#pragma unroll
-      for (int m = 1; m < 64; m <<= 1) q += __shfl_xor(q, m);
-      s1[k] = s;
-      m2[k] = q;
-    }
-    if (lane < 8 && c + lane < p.C) {
-      float a = 0.f, b = 0.f;
-#pragma unroll
-      for (int k = 0; k < 8; ++k)
-        if (k == lane) { a = s1[k]; b = m2[k]; }
-      float* so = p.stats + (long)tile * 2 * p.stats_ld;
-      so[c + lane] = a;
-      so[p.stats_ld + c + lane] = b;
-    }
-    if (blockIdx.y == 0 && threadIdx.x == 0) p.stats_cnt[tile] = (float)(vy * vx);
+    wait_vmcnt<0>();
+    __syncthreads();
   }
 }
 
@@ -327,11 +419,29 @@ static int dw_tiles(const yms_dw_shape* s, int& tx, int& ty) {
   return s->n * tx * ty;
 }
 
+// forward / dgrad grid: image column tiles split into strips of tps tiles; strips are split only
+// as far as needed for about 2048 blocks (8 per CU), longer strips re-read fewer halo rows
+static dim3 dw_strip_grid(const yms_dw_shape* s, DwParams& p) {
+  dw_tiles(s, p.tiles_x, p.tiles_y);
+  const long cg = (s->c + DW_CB - 1) / DW_CB;
+  const long base = (long)s->n * p.tiles_x * cg;
+  const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (2048 + base - 1) / base));
+  p.tps = (p.tiles_y + want - 1) / want;
+  p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
+  return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
+}
+
 static bool dw_shape_ok(const yms_dw_shape* s) {
   return s && s->n > 0 && s->h > 0 && s->w > 0 && s->c > 0 && s->c % 8 == 0 && (s->k == 3 || s->k == 5 || s->k == 7 || s->k == 9) &&
          s->dtype >= 0 && s->dtype <= 2 && (long)s->n * s->h * s->w < (1l << 31);
 }
 static bool dw_view_ok(int ld, int off, int c) { return ld % 8 == 0 && off % 8 == 0 && off + c <= ld; }
+// forward / dgrad read one image through a raw buffer resource: 32-bit byte offsets below the
+// out-of-range marker NT_OOB
+static bool dw_image_fits(const yms_dw_shape* s, int ld) {
+  const long esz = s->dtype == YMS_F32 ? 4 : 2;
+  return (long)s->h * s->w * ld * esz < (long)NT_OOB;
+}
 
 // spatial partitions of the wgrad grid: about 1024 blocks in total over the channel groups (two
 // 512-thread blocks fit a CU), each walking several tiles so the ws rows stay few
@@ -393,14 +503,14 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   if (!dw_shape_ok(s) || !x || !w || !y || !dw_view_ok(x_ld, x_off, s->c) || !dw_view_ok(y_ld, y_off, s->c))
     return YMS_ERR_INVALID;
   if (stats && stats_ld < s->c) return YMS_ERR_INVALID;
+  if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
   DwParams p{};
   p.src = (const char*)x; p.src_ld = x_ld; p.src_off = x_off; p.w = w;
   p.dst = (char*)y; p.dst_ld = y_ld; p.dst_off = y_off;
   p.scale = scale; p.shift = shift; p.act = act; p.stats = stats; p.stats_ld = stats_ld;
   if (stats) p.stats_cnt = stats + (long)yms_dwconv_stats_rows(s) * 2 * stats_ld;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  const int tiles = dw_tiles(s, p.tiles_x, p.tiles_y);
-  dim3 grid((unsigned)tiles, (unsigned)((s->c + DW_CB - 1) / DW_CB));
+  const dim3 grid = dw_strip_grid(s, p);
   hipStream_t st = (hipStream_t)stream;
   YMS_DW_T(s->dtype, YMS_DW_K(s->k, {
     if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_STATS>), grid, dim3(256), 0, st, p);
@@ -413,12 +523,12 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
                             int dx_ld, int dx_off, int accumulate, void* stream) {
   if (!dw_shape_ok(s) || !dz || !w || !dx || !dw_view_ok(dz_ld, dz_off, s->c) || !dw_view_ok(dx_ld, dx_off, s->c))
     return YMS_ERR_INVALID;
+  if (!dw_image_fits(s, dz_ld)) return YMS_ERR_UNSUPPORTED;
   DwParams p{};
   p.src = (const char*)dz; p.src_ld = dz_ld; p.src_off = dz_off; p.w = w;
   p.dst = (char*)dx; p.dst_ld = dx_ld; p.dst_off = dx_off; p.accumulate = accumulate;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  const int tiles = dw_tiles(s, p.tiles_x, p.tiles_y);
-  dim3 grid((unsigned)tiles, (unsigned)((s->c + DW_CB - 1) / DW_CB));
+  const dim3 grid = dw_strip_grid(s, p);
   hipStream_t st = (hipStream_t)stream;
   YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_DGRAD>), grid, dim3(256), 0, st, p)));
   return launch_status();

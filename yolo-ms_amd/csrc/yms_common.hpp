@@ -110,6 +110,16 @@ __device__ __forceinline__ void unpack8(const Raw8<T>& r, float (&f)[8]) {
 #pragma unroll
   for (int i = 0; i < 8; ++i) f[i] = (float)t[i];
 }
+// bf16 -> fp32 is a 16-bit shift: done on the 32-bit words, so the 16-B chunk stays one value (the
+// element-wise form above lets hipcc re-split rows of chunks into u16 + misaligned b128 reads)
+template <>
+__device__ __forceinline__ void unpack8<bf16>(const Raw8<bf16>& r, float (&f)[8]) {
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    f[2 * j] = __uint_as_float(r.v[0][j] << 16);
+    f[2 * j + 1] = __uint_as_float(r.v[0][j] & 0xffff0000u);
+  }
+}
 
 // Unsigned 31-bit fast division by a runtime constant (Granlund-Montgomery).
 struct FastDiv {
