@@ -44,10 +44,16 @@ struct DwParams {
   int ysplit, tps;       // forward / dgrad: strips per image column of tiles, tiles per strip
 };
 
+// LDS row stride (16-B chunks) for rows of n chunks: one chunk of padding when n is a multiple
+// of 4 (a 64-B multiple: rows read by one wave's lanes would start in the same banks); other
+// widths already stagger (k = 3 and 7 halos), and the k = 3 ring must stay at 4 blocks per CU
+constexpr int dw_rs(int n) { return n % 4 == 0 ? n + 1 : n; }
+
 // stage the (TY + K - 1) x (TX + K - 1) halo of 32 channels (zero outside the image / past C)
+// into rows of dw_rs(HW) chunks
 template <typename T, int K, int NT = 256>
 __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, int n, int y0, int x0, int c0) {
-  constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1, P = K / 2;
+  constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1, P = K / 2, RS = dw_rs(HW);
   const T* src = reinterpret_cast<const T*>(p.src);
   for (int it = threadIdx.x; it < DW_G * HH * HW; it += NT) {
     const int g = it / (HH * HW), r = it - g * (HH * HW);
@@ -58,7 +64,7 @@ __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, i
     for (int k = 0; k < (int)(sizeof(T) / 2); ++k) v.v[k] = u32x4{0u, 0u, 0u, 0u};
     if (y >= 0 && y < p.H && x >= 0 && x < p.W && c < p.C)
       load_raw8(src + (((long)n * p.H + y) * p.W + x) * p.src_ld + p.src_off + c, min(8, p.C - c), v);
-    lds[it] = v;
+    lds[(g * HH + hy) * RS + hx] = v;
   }
 }
 
@@ -112,7 +118,8 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
   constexpr int P = K / 2, HW = DW_TX + K - 1, RB = 2 * DW_TY + K - 1;
   // ONE __shared__ object: a second one beside the LDS-DMA target makes hipcc wait vmcnt(0) before
   // the first ds_read of every kernel row (cdna_hip_programming.md, .s-level trap (a))
-  constexpr int RING_B = DW_G * RB * HW * (int)sizeof(Raw8<T>);
+  constexpr int RS = dw_rs(HW);   // ring row stride (chunks)
+  constexpr int RING_B = DW_G * RB * RS * (int)sizeof(Raw8<T>);
   constexpr int WL_B = DW_G * K * K * 8 * (int)sizeof(float);
   __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + DW_G * 16 * (int)sizeof(float)];
   Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
@@ -159,8 +166,8 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
   const i32x4 rs = {(int)(uint32_t)ib, (int)(uint32_t)(ib >> 32) & 0xffff,
                     (int)((long)p.H * p.W * p.src_ld * (long)sizeof(T)), NT_RSRC3};
   const uint32_t myring = __builtin_amdgcn_readfirstlane(
-      (uint32_t)reinterpret_cast<uintptr_t>(ring + g * RB * HW));   // LDS byte address (wave-uniform)
-  constexpr uint32_t ROWB = HW * (uint32_t)sizeof(Raw8<T>);
+      (uint32_t)reinterpret_cast<uintptr_t>(ring + g * RB * RS));   // LDS byte address (wave-uniform)
+  constexpr uint32_t ROWB = RS * (uint32_t)sizeof(Raw8<T>);
   // prologue: the first tile's TY + K - 1 rows
   for (int hy = 0; hy < DW_TY + K - 1; ++hy)
     dw_row_dma<T, K>(rs, myring + ((t0 * DW_TY + hy) % RB) * ROWB, t0 * DW_TY - P + hy, x0, c, p.H, p.W, p.C,
@@ -178,7 +185,7 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
         sl = sl + 1 == RB ? 0 : sl + 1;
       }
     }
-    const Raw8<T>* hp = ring + g * RB * HW + 4 * qx;
+    const Raw8<T>* hp = ring + g * RB * RS + 4 * qx;
     float acc[DW_RX][8];
 #pragma unroll
     for (int i = 0; i < DW_RX; ++i)
@@ -196,7 +203,7 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
 #pragma unroll
         for (int k = 0; k < 4; ++k) { wr[dx][k] = a[k]; wr[dx][4 + k] = b[k]; }
       }
-      const Raw8<T>* row = hp + slot * HW;
+      const Raw8<T>* row = hp + slot * RS;
 #pragma unroll
       for (int q = 0; q < DW_RX + K - 1; ++q) {
         float v[8];
@@ -309,8 +316,10 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1;
   constexpr int S = DwWg<K>::S, SL = DwWg<K>::SL, NA = DwWg<K>::NA;
   static_assert(NA <= DW_WG_LPG && SL % 4 == 0, "dw wgrad lane mapping");
-  constexpr int HALO = DW_G * HH * HW, DZN = DW_G * DW_TY * DW_TX;
-  constexpr int STAGE_B = (HALO + DZN) * (int)sizeof(Raw8<T>);
+  constexpr int HRS = dw_rs(HW), DRS = dw_rs(DW_TX);   // padded LDS row strides (chunks)
+  constexpr int HALO = DW_G * HH * HRS, DZN = DW_G * DW_TY * DW_TX;
+  constexpr int DZL = DW_G * DW_TY * DRS;
+  constexpr int STAGE_B = (HALO + DZL) * (int)sizeof(Raw8<T>);
   constexpr int RED_B = NA * K * 8 * (int)sizeof(float);
   __shared__ __attribute__((aligned(16))) char smem[STAGE_B > RED_B ? STAGE_B : RED_B];
   Raw8<T>* halo = reinterpret_cast<Raw8<T>*>(smem);
@@ -342,12 +351,12 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
       for (int k = 0; k < (int)(sizeof(T) / 2); ++k) v.v[k] = u32x4{0u, 0u, 0u, 0u};
       if (y < p.H && x < p.W && c < p.C)
         load_raw8(dzp + (((long)n * p.H + y) * p.W + x) * dz_ld + dz_off + c, min(8, p.C - c), v);
-      dzl[it] = v;
+      dzl[(g2 * DW_TY + r2 / DW_TX) * DRS + r2 % DW_TX] = v;
     }
     __syncthreads();
     if (active) {
-      const Raw8<T>* hrow = halo + g * HH * HW + (ty + dy) * HW + sx;
-      const Raw8<T>* drow = dzl + g * DW_TY * DW_TX + ty * DW_TX + sx;
+      const Raw8<T>* hrow = halo + (g * HH + ty + dy) * HRS + sx;
+      const Raw8<T>* drow = dzl + (g * DW_TY + ty) * DRS + sx;
 #pragma unroll 2
       for (int x4 = 0; x4 < SL; x4 += 4) {
         float d[4][8];
