@@ -29,7 +29,7 @@ def _ref(z, gy, sc, sh, mu, istd, act):
 
 
 @pytest.mark.parametrize("npix,c,act", [(44800, 64, 1), (57600, 32, 1), (40001, 24, 0), (100, 16, 1),
-                                        (7 * 80 * 80, 128, 1)])
+                                        (7 * 80 * 80, 128, 1), (25600, 768, 1), (3000, 1152, 0)])
 def test_bn_bwd_matches_fp64(npix, c, act):
     g = torch.Generator().manual_seed(npix + c)
     z = torch.randn(npix, c, generator=g, dtype=torch.float64)

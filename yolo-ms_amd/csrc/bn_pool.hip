@@ -854,6 +854,8 @@ yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count,
                                    float* dbeta, float* coef, void* stream) {
   if (c <= 0 || !ws || rows <= 0 || count <= 0) return YMS_ERR_INVALID;
   static const int wide = getenv("YMS_BN_FIN_1024") ? atoi(getenv("YMS_BN_FIN_1024")) : 0;   // dev A/B
+  // (tried: float4 channel quads x 32 row lanes with every load of a lane in flight at once --
+  // the step got slower, 19.42 -> 19.65 ms interleaved; the finalize is not load-latency bound)
   if (wide)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, ws,
                        rows, count, dgamma, dbeta, coef);

@@ -1376,6 +1376,20 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   // pixels per split
   static const int wpc = getenv("YMS_WG_WPC") ? std::max(1, atoi(getenv("YMS_WG_WPC"))) : 4;
   int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(wpc * cu_count(), blocks)));
+  // deep layers: every split writes (and the reduce re-reads) a full fp32 slab of the weight
+  // gradient, which can exceed the layer's own x + dz bytes several times over.  Cap the slab
+  // round trip at `ratio` x the algorithmic bytes, keeping at least `min_blocks` workgroups.
+  // (interleaved A/B, YOLOv8-s step: off 19.71/19.71/19.81 ms, ratio 1 19.62/19.64/19.76 ms;
+  // YOLO-MS-S 40.11/40.12 -> 40.04/40.02 ms -- the wgrads run on the side stream, so the
+  // step gains only the HBM contention the slabs caused)
+  static const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 1.0;
+  static const int min_blocks = getenv("YMS_WG_MIN_BLOCKS") ? std::max(1, atoi(getenv("YMS_WG_MIN_BLOCKS"))) : 256;
+  if (ratio > 0.0) {
+    const double data = (double)M * (double)(rup(s->cout, 8) + w.cin8) * es;
+    const double slab_rt = 2.0 * 4.0 * (double)w.slab_rows * (double)w.slab_ld;
+    const int cap = std::max((int)(ratio * data / slab_rt), cdiv(min_blocks, blocks));
+    splits = std::max(1, std::min(splits, cap));
+  }
   w.kt_per_split = cdiv(w.nkt, splits);
   w.splits = cdiv(w.nkt, w.kt_per_split);
   return w;

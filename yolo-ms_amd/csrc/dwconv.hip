@@ -434,7 +434,8 @@ static dim3 dw_strip_grid(const yms_dw_shape* s, DwParams& p) {
   dw_tiles(s, p.tiles_x, p.tiles_y);
   const long cg = (s->c + DW_CB - 1) / DW_CB;
   const long base = (long)s->n * p.tiles_x * cg;
-  const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (2048 + base - 1) / base));
+  static const long target = getenv("YMS_DW_BLOCKS") ? std::max(1, atoi(getenv("YMS_DW_BLOCKS"))) : 2048;   // dev A/B
+  const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (target + base - 1) / base));
   p.tps = (p.tiles_y + want - 1) / want;
   p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
   return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
