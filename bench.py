@@ -116,14 +116,27 @@ def add_traffic(roof, mode, workload):
 
 
 def conv_roofline(prof, label):
-    calls = sum(v[0] for k, v in prof.items() if k.startswith("yms_conv_") and v[2])
-    ms = sum(v[1] for k, v in prof.items() if k.startswith("yms_conv_") and v[2])
-    fl = sum(v[2] for k, v in prof.items() if k.startswith("yms_conv_"))
+    rows = [v for k, v in prof.items() if k.startswith("yms_conv_") and v[2]]
+    calls = sum(v[0] for v in rows)
+    ms = sum(v[1] for v in rows)
+    fl = sum(v[2] for v in rows)
+    nb = sum(v[3] for v in rows)
+    t_roof = sum(v[4] for v in rows)
     ach = fl / (ms * 1e-3) / 1e12 if ms > 0 else 0.0
     return {"bound": "mfma", "achieved": round(ach, 2), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
             "frac": round(ach / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None, "kernel": label,
             "launches": calls, "avg_launch_us": round(ms * 1e3 / max(calls, 1), 2),
-            "algorithmic_gflop_per_launch": round(fl / max(calls, 1) / 1e9, 3)}
+            "algorithmic_gflop_per_launch": round(fl / max(calls, 1) / 1e9, 3),
+            # per-launch roofline of each layer's own arithmetic intensity, min(MFMA peak,
+            # AI x HBM peak): sum over launches of max(flops / 2.5 PF, bytes / 8 TB/s) against the
+            # measured time; bytes = input + output + weights once per launch (algorithmic)
+            "per_layer_roofline": {
+                "t_attainable_ms": round(t_roof, 4), "t_measured_ms": round(ms, 4),
+                "frac": round(t_roof / ms, 4) if ms > 0 else 0.0,
+                "hbm_bound_launches": sum(v[5] for v in rows),
+                "algorithmic_mb_per_launch": round(nb / max(calls, 1) / 1e6, 2),
+                "achieved_hbm_gb_s": round(nb / (ms * 1e-3) / 1e9, 1) if ms > 0 else 0.0,
+                "peak_hbm_gb_s": HBM_PEAK_GBS}}
 
 
 class MeanSquare(torch.autograd.Function):

@@ -14,6 +14,12 @@
  *   greedily keep i; suppress j if inter/(area_i+area_j-inter) > iou_threshold,
  *   inter = max(0,xx2-xx1)*max(0,yy2-yy1), the fp32 ratio promoted to double for the
  *   compare (iou_threshold is a double in the CPU kernel).
+ *   max / min are std::max / std::min, restated literally: std::max(a, b) = (a < b) ? b : a,
+ *   std::min(a, b) = (b < a) ? b : a -- on a NaN operand they return the FIRST argument, where
+ *   C's fmaxf / fminf (and the GPU's v_max_f32 / v_min_f32) return the non-NaN one.  The
+ *   suppression decisions cannot differ: a NaN coordinate of box i (j) makes area_i (area_j)
+ *   NaN, so the ratio is NaN under either semantics and NaN > iou is false
+ *   (tests/test_nms_gpu.py's NaN-coordinate case checks the GPU against this literal form).
  * PARITY UNPINNED for NMS: no reference test or fixture pins NMS output; the oracle is
  * checked by known-answer tests (tests/test_nms_oracle.py).
  *
@@ -25,6 +31,9 @@
 #include <string.h>
 
 typedef struct { float s; int64_t i; } sk_t;
+
+static inline float std_max(float a, float b) { return (a < b) ? b : a; }
+static inline float std_min(float a, float b) { return (b < a) ? b : a; }
 
 static int cmp_desc_stable(const void* a, const void* b) {
   const sk_t* x = (const sk_t*)a;
@@ -58,12 +67,12 @@ int64_t yms_ref_nms(const float* boxes, const float* scores, int64_t n, double i
     for (int64_t _j = _i + 1; _j < n; ++_j) {
       int64_t j = order[_j].i;
       if (sup[j]) continue;
-      const float xx1 = fmaxf(ix1, boxes[4 * j]);
-      const float yy1 = fmaxf(iy1, boxes[4 * j + 1]);
-      const float xx2 = fminf(ix2, boxes[4 * j + 2]);
-      const float yy2 = fminf(iy2, boxes[4 * j + 3]);
-      const float w = fmaxf(0.0f, xx2 - xx1);
-      const float h = fmaxf(0.0f, yy2 - yy1);
+      const float xx1 = std_max(ix1, boxes[4 * j]);
+      const float yy1 = std_max(iy1, boxes[4 * j + 1]);
+      const float xx2 = std_min(ix2, boxes[4 * j + 2]);
+      const float yy2 = std_min(iy2, boxes[4 * j + 3]);
+      const float w = std_max(0.0f, xx2 - xx1);
+      const float h = std_max(0.0f, yy2 - yy1);
       const float inter = w * h;
       const float ovr = inter / (iarea + areas[j] - inter);
       if ((double)ovr > iou_thr) sup[j] = 1;

@@ -184,6 +184,13 @@ def test_big_segment_grid_edge_cases():
     p = seg(8, 40)
     p[0, 123, 0] = np.nan
     _check(p, 0.25, 0.5)
+    # NaN coordinates on the top-scoring box (the kept box i of the std::max/min restatement)
+    # and scattered NaN widths / heights: the oracle uses std::max/min, the GPU IEEE max/min
+    p = seg(8, 40)
+    p[0, int(np.argmax(p[0, :, 4])), 2] = np.nan
+    p[0, 5::61, 3] = np.nan
+    p[0, 9::83, 1] = np.nan
+    _check(p, 0.25, 0.5)
     p = seg(8, 40)
     p[0, 77, 1] = np.inf
     _check(p, 0.25, 0.5)

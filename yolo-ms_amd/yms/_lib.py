@@ -149,11 +149,15 @@ def call(name, *args):
     s.record(st)
     check(getattr(lib(), name)(*args), name)
     e.record(st)
-    fl = 0
+    fl = nb = 0
     if name in _CONV:
         sh = args[0].contents
         fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
-    _prof.append((name, s, e, fl))
+        # algorithmic HBM bytes: each operand once (input, output, weights; fp32 weight gradient)
+        es = 4 if sh.dtype == F32 else 2
+        act = (sh.n * sh.h * sh.w * sh.cin + sh.n * sh.ho * sh.wo * sh.cout) * es
+        nb = act + sh.cout * sh.cin * sh.k * sh.k * (4 if name == "yms_conv_wgrad" else es)
+    _prof.append((name, s, e, fl, nb))
 
 
 def profile_begin():
@@ -163,16 +167,22 @@ def profile_begin():
     _prof = []
 
 
-def profile_end():
-    """-> {name: [calls, total_ms, flops]} for the launches since profile_begin()."""
+def profile_end(peak_tflops=2500.0, peak_gbs=8000.0):
+    """-> {name: [calls, total_ms, flops, bytes, roofline_ms, hbm_bound_calls]} for the launches
+    since profile_begin().  roofline_ms sums, per launch, max(flops / peak_tflops, bytes /
+    peak_gbs): the time the launch would take at the roofline of its own arithmetic intensity."""
     global _prof
     torch.cuda.synchronize()
     out = {}
-    for name, s, e, fl in _prof:
-        r = out.setdefault(name, [0, 0.0, 0])
+    for name, s, e, fl, nb in _prof:
+        r = out.setdefault(name, [0, 0.0, 0, 0, 0.0, 0])
         r[0] += 1
         r[1] += s.elapsed_time(e)
         r[2] += fl
+        r[3] += nb
+        t_f, t_b = fl / (peak_tflops * 1e9), nb / (peak_gbs * 1e6)   # ms
+        r[4] += max(t_f, t_b)
+        r[5] += int(t_b > t_f)
     _prof = None
     return out
 
