@@ -46,6 +46,8 @@ def parse():
                     help="compute: the reference's ComputeLoss semantics on the GPU (loss.py:94-677) with "
                          "synthetic targets; surrogate: sum of mean(o^2) over the head maps")
     ap.add_argument("--gts", type=int, default=8, help="synthetic ground-truth boxes per image (--loss compute)")
+    ap.add_argument("--ms-version", default="ms-s",
+                    help="also time this YOLO-MS (MS-Block / HKS) graph at 1 GPU ('none': skip)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-profile", action="store_true")
     ap.add_argument("--mode", default="both", choices=["both", "train", "infer"])
@@ -256,6 +258,62 @@ def cpu_baseline_infer(version, nc, size, batch=8, steps=12):
             f"({dt:.1f} s), torch threads={threads}"}
 
 
+def measure_ms_family(a, dev, dtype):
+    """The MS-Block / HKS graph of the same size class (the reference holds it only as
+    a diagram, so these lines are not oracle-pinned like configs[2]): training step with the GPU
+    ComputeLoss at the same per-GPU batch, and inference + NMS at the configs[1] batch."""
+    from yms import set_compute_dtype
+    from yms import ops as yops
+    from yolov8.tools.loss import ComputeLoss
+    from yolov8.yolov8 import YOLOv8
+
+    steps, warmup = min(a.steps, 40), min(a.warmup, 10)
+    out = {"version": a.ms_version, "steps": steps, "warmup": warmup}
+    torch.manual_seed(0)
+    m = YOLOv8(a.ms_version, a.nc).to(dev)
+    m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    set_compute_dtype(m, dtype)
+    if a.mode in ("both", "train"):
+        m.train()
+        opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.937, nesterov=True, weight_decay=5e-4,
+                              foreach=True)
+        x = torch.randn(a.batch, 3, a.size, a.size, device=dev, generator=torch.Generator(device=dev).manual_seed(7))
+        crit = ComputeLoss(m.head, a.nc, dev, (a.size, a.size))
+        tg = synth_targets(a.batch, a.nc, a.gts, 4321, dev)
+
+        def step():
+            opt.zero_grad(set_to_none=True)
+            crit.loss_tensor(m(x), tg)[0].backward()
+            opt.step()
+
+        dt, med = timed(step, steps, warmup, 1)
+        out["train"] = {"value": round(a.batch * steps / dt, 2), "unit": "images/sec",
+                        "ms_per_step": round(dt / steps * 1e3, 3), "ms_per_step_median": round(med, 3),
+                        "workload": f"{a.ms_version} {a.size}x{a.size} {a.dtype} training, B={a.batch}, "
+                                    "fwd+ComputeLoss+bwd+SGD-nesterov step"}
+        log(f"[rank 0] {a.ms_version} train: {out['train']['value']} img/s")
+        del opt, x
+    if a.mode in ("both", "infer") and not a.no_infer:
+        torch.manual_seed(0)
+        mi = YOLOv8(a.ms_version, a.nc).to(dev).eval()
+        mi.head.stride = torch.tensor([8.0, 16.0, 32.0])
+        set_compute_dtype(mi, dtype)
+        xi = torch.randn(a.infer_batch, 3, a.size, a.size, device=dev,
+                         generator=torch.Generator(device=dev).manual_seed(99))
+
+        def istep():
+            yops.batched_nms_indices(mi(xi), 0.25, 0.45)
+
+        dti, medi = timed(istep, steps, warmup, 1)
+        out["infer"] = {"value": round(a.infer_batch * steps / dti, 2), "unit": "images/sec",
+                        "ms_per_batch": round(dti / steps * 1e3, 3), "ms_per_batch_median": round(medi, 3),
+                        "workload": f"{a.ms_version} {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} "
+                                    "(forward + decode + class-wise NMS)"}
+        log(f"[rank 0] {a.ms_version} infer: {out['infer']['value']} img/s")
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     a = parse()
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -356,6 +414,9 @@ def main():
             infer_step()
             result["infer_prof"] = _lib.profile_end()
 
+    if rank == 0 and world == 1 and a.ms_version != "none" and not a.version.startswith("ms-"):
+        result["ms"] = measure_ms_family(a, dev, dtype)
+
     if rank == 0:
         from oracle import model_ref as M
         if a.version.startswith("ms-"):
@@ -417,6 +478,8 @@ def main():
                 line["ms_per_step"] = inf["ms_per_batch"]
                 line["config"] = {"workload": inf["workload"], "global_batch": a.infer_batch, "img": a.size,
                                   "parallelism": "replica"}
+        if "ms" in result:
+            line["ms_family"] = result["ms"]
         if world == 1 and not a.no_cpu_baseline:
             log("[rank 0] cpu baseline (oracle on host cores)...")
             if "train" in result:

@@ -96,6 +96,17 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
                         const void* wpacked, void* y, int y_ld, int y_off,
                         const float* scale, const float* shift, int act,
                         const void* res, int res_ld, int res_off, float* stats, void* stream);
+/* Stem convolution (yolov8_backbone.py:30-40, the backbone's first Conv(cin, c1, 3, 2, 1), replacing
+ * the NHWC input pack + yms_conv_fwd pair): x is the model's NCHW fp32 input [n][cin][h][w], w the
+ * fp32 nn.Conv2d weight [cout][cin][3][3] (rounded to s->dtype in the kernel, as the packing
+ * does).  Supported: yms_conv_stem_supported(s) (cin 1..3, k 3, stride 2, pad 1, cout % 8 == 0,
+ * cout <= 96, bf16 / f16).  Same epilogues as yms_conv_fwd without the residual; statistics:
+ * yms_conv_stem_stats_rows(s) rows (one per 8 x 32 output tile), counts after the rows. */
+int yms_conv_stem_supported(const yms_conv_shape* s);
+int yms_conv_stem_stats_rows(const yms_conv_shape* s);
+yms_status yms_conv_stem_fwd(const yms_conv_shape* s, const float* x, const float* w, void* y, int y_ld,
+                             int y_off, const float* scale, const float* shift, int act, float* stats,
+                             int stats_ld, void* stream);
 /* dx (+)= conv_transpose(dz, W) with wpacked_t = yms_conv_pack_weight(.., for_dgrad=1). */
 yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
                           const void* wpacked_t, void* dx, int dx_ld, int dx_off,

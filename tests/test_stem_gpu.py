@@ -1,0 +1,129 @@
+"""Stem convolution (yms_conv_stem_fwd: NCHW fp32 input -> NHWC, 3x3 stride 2, cin <= 3) against
+torch fp32 on the dtype-rounded operands, and the model with the stem path against the generic
+pack + implicit-GEMM path (YMS_STEM=0).  Reference layer: yolov8/model/yolov8_backbone.py:30-40
+(Conv(in_channels, int(64*w), 3, 2, 1) -> BN -> SiLU, components.py:69-77)."""
+import ctypes
+import os
+import sys
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+sys.path.insert(0, os.path.dirname(__file__))
+from hiputil import DT, r8, shape  # noqa: E402
+from yms import _lib as L  # noqa: E402
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref(x, w, dt):
+    """conv of the dtype-rounded operands in fp32 (the kernel's products are exact)."""
+    xr = x.to(DT[dt]).float()
+    wr = w.to(DT[dt]).float()
+    return F.conv2d(xr, wr, stride=2, padding=1)
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("n,h,w,cin,cout", [(2, 64, 64, 3, 32), (3, 37, 70, 3, 48), (1, 130, 66, 2, 16),
+                                            (2, 40, 40, 1, 80), (1, 17, 9, 3, 96)])
+def test_stem_eval_affine_silu(dt, n, h, w, cin, cout):
+    g = torch.Generator().manual_seed(n * 1000 + h + cout)
+    x = torch.randn(n, cin, h, w, generator=g) * 2.0
+    wt = torch.randn(cout, cin, 3, 3, generator=g) * 0.3
+    sc = torch.rand(cout, generator=g) + 0.5
+    sh = torch.randn(cout, generator=g) * 0.2
+    sh_ = shape(n, h, w, cin, cout, 3, 2, DT[dt])
+    sp = ctypes.pointer(sh_)
+    assert L.lib().yms_conv_stem_supported(sp) == 1
+    ld = r8(cout) + 8                     # a wider buffer: the output is a channel slot (off 8)
+    y = torch.full((n, sh_.ho, sh_.wo, ld), float("nan"), dtype=DT[dt], device="cuda")
+    xd, wd = x.cuda(), wt.cuda()
+    scd, shd = sc.cuda(), sh.cuda()
+    L.call("yms_conv_stem_fwd", sp, xd.data_ptr(), wd.data_ptr(), y.data_ptr(), ld, 8, scd.data_ptr(),
+           shd.data_ptr(), L.ACT_SILU, None, 0, L.stream_ptr())
+    torch.cuda.synchronize()
+    ref = F.silu(_ref(x, wt, dt) * sc[:, None, None] + sh[:, None, None])
+    out = y[..., 8:8 + cout].permute(0, 3, 1, 2).float().cpu()
+    assert torch.isnan(y[..., :8].float()).all()          # channels outside the slot untouched
+    tol = 8e-3 if dt == "bf16" else 1e-3
+    err = (out - ref).abs().max().item()
+    assert err <= tol * max(1.0, ref.abs().max().item()), err
+
+
+@pytest.mark.parametrize("n,h,w,cout", [(2, 64, 64, 32), (3, 45, 77, 48)])
+def test_stem_training_z_and_statistics(n, h, w, cout):
+    dt = "bf16"
+    g = torch.Generator().manual_seed(h * w + cout)
+    x = torch.randn(n, 3, h, w, generator=g) + 3.0      # |mean| >> std: centred moments matter
+    wt = torch.randn(cout, 3, 3, 3, generator=g) * 0.3
+    sh_ = shape(n, h, w, 3, cout, 3, 2, DT[dt])
+    sp = ctypes.pointer(sh_)
+    rows = L.lib().yms_conv_stem_stats_rows(sp)
+    ld_s = L.lib().yms_conv_stats_ld(sp)
+    assert rows == n * ((sh_.ho + 7) // 8) * ((sh_.wo + 31) // 32)
+    stats = torch.full((rows * (2 * ld_s + 1),), float("nan"), device="cuda")
+    z = torch.empty((n, sh_.ho, sh_.wo, r8(cout)), dtype=DT[dt], device="cuda")
+    xd, wd = x.cuda(), wt.cuda()
+    L.call("yms_conv_stem_fwd", sp, xd.data_ptr(), wd.data_ptr(), z.data_ptr(), r8(cout), 0, None, None,
+           L.ACT_NONE, stats.data_ptr(), ld_s, L.stream_ptr())
+    npix = n * sh_.ho * sh_.wo
+    gam, bet = torch.ones(cout, device="cuda"), torch.zeros(cout, device="cuda")
+    rm, rv = torch.zeros(cout, device="cuda"), torch.ones(cout, device="cuda")
+    mi = torch.empty(2 * cout, device="cuda")
+    sc, sf = torch.empty(cout, device="cuda"), torch.empty(cout, device="cuda")
+    L.call("yms_bn_finalize", cout, stats.data_ptr(), rows, ld_s, npix, gam.data_ptr(), bet.data_ptr(),
+           rm.data_ptr(), rv.data_ptr(), ctypes.c_float(0.03), ctypes.c_float(1e-3), mi.data_ptr(),
+           sc.data_ptr(), sf.data_ptr(), L.stream_ptr())
+    torch.cuda.synchronize()
+    ref = _ref(x, wt, dt).double()
+    zz = z[..., :cout].permute(0, 3, 1, 2).double().cpu()
+    assert (zz - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    # statistics are of the fp32 accumulators (as the implicit-GEMM epilogue's)
+    mean = ref.mean((0, 2, 3))
+    var = ref.var((0, 2, 3), unbiased=False)
+    assert torch.allclose(mi[:cout].double().cpu(), mean, rtol=1e-5, atol=1e-4 * mean.abs().max().item())
+    istd = 1.0 / (var + 1e-3).sqrt()
+    assert torch.allclose(mi[cout:].double().cpu(), istd, rtol=2e-4)
+    cnt = stats[rows * 2 * ld_s:].cpu()
+    assert cnt.sum().item() == npix
+
+
+def test_stem_rejects_unsupported():
+    sp = ctypes.pointer(shape(2, 64, 64, 4, 32, 3, 2, torch.bfloat16))      # cin 4
+    assert L.lib().yms_conv_stem_supported(sp) == 0
+    sp = ctypes.pointer(shape(2, 64, 64, 3, 32, 3, 1, torch.bfloat16))      # stride 1
+    assert L.lib().yms_conv_stem_supported(sp) == 0
+    sp = ctypes.pointer(shape(2, 64, 64, 3, 32, 3, 2, torch.float32))       # fp32: generic path
+    assert L.lib().yms_conv_stem_supported(sp) == 0
+    x = torch.zeros(1, device="cuda")
+    assert L.lib().yms_conv_stem_fwd(sp, x.data_ptr(), x.data_ptr(), x.data_ptr(), 32, 0, None, None, 0, None, 0,
+                                     None) != 0
+
+
+@pytest.mark.parametrize("v,training", [("n", False), ("s", True), ("ms-xs", True)])
+def test_model_stem_path_matches_generic_path(v, training, monkeypatch):
+    from yms import set_compute_dtype
+    from yolov8.yolov8 import YOLOv8
+
+    torch.manual_seed(0)
+    x = torch.randn(2, 3, 96, 128, device="cuda")
+    outs = {}
+    for stem in ("1", "0"):
+        monkeypatch.setenv("YMS_STEM", stem)
+        torch.manual_seed(1)
+        m = YOLOv8(v, 80).cuda()
+        set_compute_dtype(m, torch.bfloat16)
+        m.train(training)
+        if not training:
+            m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+            outs[stem] = (m(x).float(),)
+        else:
+            o = m(x)
+            sum((t.float() ** 2).mean() for t in o).backward()
+            outs[stem] = tuple(t.float() for t in o) + (m.backbone.conv0.conv.weight.grad.clone(),)
+        plans = list(m.__dict__["_yms_plans"].values())
+        assert sum(len(p.stem_inputs) for p in plans) == (1 if stem == "1" else 0)
+    for a, b in zip(outs["1"], outs["0"]):
+        err = ((a - b).norm() / b.norm()).item()
+        assert err < 2e-2, err

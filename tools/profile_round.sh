@@ -16,7 +16,7 @@ mkdir -p "$OUT"
 cd /tmp && export TMPDIR=/tmp
 for mode in $MODES; do
   timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/stats_$mode" -o run -- \
-    python3 "$ROOT/bench.py" --mode $mode --steps 10 --warmup 3 --no-cpu-baseline $EXTRA > "$OUT/bench_$mode.json" 2> "$OUT/bench_$mode.err"
+    python3 "$ROOT/bench.py" --mode $mode --steps 10 --warmup 3 --no-cpu-baseline --ms-version none $EXTRA > "$OUT/bench_$mode.json" 2> "$OUT/bench_$mode.err"
 done
 echo "stats done"
 # PMC passes per mode (FETCH_SIZE and WRITE_SIZE do not fit one TCC pass on gfx950)
@@ -24,7 +24,7 @@ for mode in $MODES; do
   for c in FETCH_SIZE WRITE_SIZE "SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE SQ_BUSY_CYCLES"; do
     d=pmc_${mode}_$(echo "$c" | cut -d' ' -f1 | tr 'A-Z' 'a-z')
     timeout -k 10 600 rocprofv3 --pmc $c --output-format csv -d "$OUT/$d" -o run -- \
-      python3 "$ROOT/bench.py" --mode $mode --steps 2 --warmup 1 --no-cpu-baseline --no-profile $EXTRA \
+      python3 "$ROOT/bench.py" --mode $mode --steps 2 --warmup 1 --no-cpu-baseline --no-profile --ms-version none $EXTRA \
       > "$OUT/$d.json" 2> "$OUT/$d.err"
     echo "pmc $mode $c done"
   done

@@ -61,6 +61,9 @@ _SIGS = {
     "yms_conv_stats_rows": (_I, [_SP]),
     "yms_conv_stats_ld": (_I, [_SP]),
     "yms_conv_fwd": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _P]),
+    "yms_conv_stem_supported": (_I, [_SP]),
+    "yms_conv_stem_stats_rows": (_I, [_SP]),
+    "yms_conv_stem_fwd": (_I, [_SP, _P, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
     "yms_conv_dgrad": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
     "yms_conv_wgrad_ws_bytes": (_SZ, [_SP]),
     "yms_conv_wgrad": (_I, [_SP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
@@ -134,7 +137,7 @@ def check(status, what):
 
 
 _prof = None
-_CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad")
+_CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd")
 
 
 def call(name, *args):

@@ -152,6 +152,7 @@ class Rt:
         self.pg_base = None      # flat fp32 param-grad arena pointer
         self.eval_base = None    # eval cache base pointer (packed weights + folded BN)
         self.prepacked = False   # training: all weight packs already issued (Plan.prepack)
+        self.stem_x = {}         # plan input index -> NCHW fp32 tensor read by a stem ConvOp
         self.main = None         # backward: torch stream objects (main, weight-gradient side stream)
         self.side = None
 
@@ -198,6 +199,7 @@ class ConvOp:
         self.pg = b.param(mod.bn, "weight")
         self.pb = b.param(mod.bn, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
+        self.stem_input = None   # plan input index when this conv reads the NCHW input directly
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -216,7 +218,10 @@ class ConvOp:
             self.sc = La.alloc(4 * c)
             self.sh = La.alloc(4 * c)
             self.mi = La.alloc(8 * c)
-            self.stats_rows = L.lib().yms_conv_stats_rows(self.sp)
+            if self.stem_input is not None:
+                self.stats_rows = L.lib().yms_conv_stem_stats_rows(self.sp)
+            else:
+                self.stats_rows = L.lib().yms_conv_stats_rows(self.sp)
             self.stats_ld = L.lib().yms_conv_stats_ld(self.sp)
             plan.need_scratch("stats", 4 * self.stats_rows * (2 * self.stats_ld + 1))
             plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
@@ -242,8 +247,14 @@ class ConvOp:
         xl, yl = x.buf.ld, y.buf.ld
         rp = rt.a(r) if r is not None else None
         rl, ro = (r.buf.ld, r.off) if r is not None else (0, 0)
+        stem = self.stem_input is not None
         if not rt.training:
             eb = rt.eval_base
+            if stem:
+                L.call("yms_conv_stem_fwd", self.sp, rt.stem_x[self.stem_input].data_ptr(),
+                       self.mod.conv.weight.data_ptr(), rt.a(y), yl, y.off, eb + self.e_sc, eb + self.e_sh,
+                       self.act, None, 0, rt.st)
+                return
             L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, eb + self.e_wp, rt.a(y), yl, y.off,
                    eb + self.e_sc, eb + self.e_sh, self.act, rp, rl, ro, None, rt.st)
             return
@@ -253,8 +264,12 @@ class ConvOp:
             L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wp, 0, rt.st)
             L.call("yms_conv_pack_weight", self.sp, m.conv.weight.data_ptr(), base + self.t_wpt, 1, rt.st)
         stats = base + rt.plan.scratch["stats"]
-        L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
-               None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
+        if stem:
+            L.call("yms_conv_stem_fwd", self.sp, rt.stem_x[self.stem_input].data_ptr(), m.conv.weight.data_ptr(),
+                   base + self.z, self.zld, 0, None, None, L.ACT_NONE, stats, self.stats_ld, rt.st)
+        else:
+            L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
+                   None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
         bn = m.bn
         L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
@@ -318,6 +333,7 @@ class BiasConvOp:
         self.pw = b.param(conv, "weight")
         self.pbias = b.param(conv, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
+        self.stem_input = None   # plan input index when this conv reads the NCHW input directly
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -635,6 +651,7 @@ class Plan:
         self.inputs, self.outputs, self.kind = inputs, outputs, kind
         self.scratch_req = {}
         self.n_counters = 0
+        self.stem_inputs = self._find_stems()
         La, Le = Layout(), Layout()
         for buf in self.bufs:
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
@@ -672,6 +689,26 @@ class Plan:
         self.pgrad_order = order
         self._eval_sig = None
         self._eval_arena = None
+
+    def _find_stems(self):
+        """Inputs whose only reader is a stem-shaped Conv (3x3 stride 2 over <= 3 channels, no
+        residual, 16-bit compute): that conv reads the NCHW fp32 input itself
+        (yms_conv_stem_fwd); eval then skips the NHWC input pack (training keeps it for the
+        conv's weight gradient).  YMS_STEM=0 keeps the generic pack + implicit-GEMM path."""
+        out = {}
+        if self.dt == L.F32 or os.environ.get("YMS_STEM", "1") == "0":
+            return out
+        for i, v in enumerate(self.inputs):
+            readers = [op for op in self.ops
+                       if any(isinstance(a, View) and a.buf is v.buf for a in vars(op).values())]
+            if len(readers) != 1 or type(readers[0]) is not ConvOp:
+                continue
+            op = readers[0]
+            if (op.x.buf is v.buf and op.x.off == 0 and op.x.c == v.c and op.res is None and v.buf.ld == r8(v.c)
+                    and L.lib().yms_conv_stem_supported(op.sp)):
+                op.stem_input = i
+                out[i] = op
+        return out
 
     def counter(self):
         """Reserve one 16-B arrival counter in the grad scratch (-> its index)."""
