@@ -218,6 +218,9 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
 /* y (+)= a + b over npix x c channels (b may be NULL); c % 8 == 0 */
 yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,
                          int b_off, void* y, int y_ld, int y_off, int accumulate, void* stream);
+/* Backward of y = a + b in one pass: ga (+)= g, gb (+)= g (acc1 / acc2: accumulate). */
+yms_status yms_add_grad2(int dtype, long npix, int c, const void* g, int g_ld, int g_off, void* ga, int ga_ld,
+                         int ga_off, int acc1, void* gb, int gb_ld, int gb_off, int acc2, void* stream);
 
 /* ---- mAP@0.5 evaluation (validate_epoch's torchmetrics call, train.py:41-47,146,152-153) ---- */
 /* GPU: per image (det_off / gt_off prefix offsets, n_images + 1 entries), rank every detection in

@@ -90,3 +90,21 @@ def test_add_views():
     _close(nchw(y, 24).cpu(), ref, 1e-2)
     L.call("yms_add_views", L.BF16, 70, 24, ab.data_ptr(), 40, 8, None, 0, 0, y.data_ptr(), 24, 0, 0, L.stream_ptr())
     assert torch.equal(nchw(y, 24).cpu(), a.to(torch.bfloat16).float())
+
+
+@pytest.mark.parametrize("acc1,acc2", [(0, 0), (1, 0), (0, 1), (1, 1)])
+def test_add_grad2_routes_into_both_addends(acc1, acc2):
+    """yms_add_grad2: the MS-Block branch-sum backward, ga (+)= g and gb (+)= g in one pass."""
+    g = torch.Generator().manual_seed(acc1 * 2 + acc2)
+    npix, c = 3001, 24
+    gy = torch.randn(npix, 40, generator=g).to(torch.bfloat16).cuda()          # a 40-wide buffer, slot at 8
+    ga = torch.randn(npix, 32, generator=g).to(torch.bfloat16).cuda()
+    gb = torch.randn(npix, 48, generator=g).to(torch.bfloat16).cuda()
+    ea = (ga[:, 0:24].float() * acc1 + gy[:, 8:32].float()).to(torch.bfloat16)
+    eb = (gb[:, 16:40].float() * acc2 + gy[:, 8:32].float()).to(torch.bfloat16)
+    rest_a, rest_b = ga[:, 24:].clone(), gb[:, :16].clone()
+    L.call("yms_add_grad2", L.BF16, npix, c, gy.data_ptr(), 40, 8, ga.data_ptr(), 32, 0, acc1, gb.data_ptr(), 48, 16,
+           acc2, L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.equal(ga[:, 0:24], ea) and torch.equal(gb[:, 16:40], eb)
+    assert torch.equal(ga[:, 24:], rest_a) and torch.equal(gb[:, :16], rest_b)

@@ -495,6 +495,28 @@ __global__ __launch_bounds__(256) void add_views_kernel(long items, int cg, cons
   }
 }
 
+// Backward of y = a + b: g -> ga (+)= g and gb (+)= g in one pass (g read once)
+template <typename T>
+__global__ __launch_bounds__(256) void add_grad2_kernel(long items, int cg, const T* g, int g_ld, int g_off, T* y1,
+                                                        int ld1, int off1, int acc1, T* y2, int ld2, int off2,
+                                                        int acc2) {
+  for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
+    const long pix = it / cg;
+    const int c = (int)(it - pix * cg) * 8;
+    float vg[8], v1[8], v2[8];
+    Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
+    if (acc1) Vec8<T>::load(y1 + pix * ld1 + off1 + c, v1);
+    if (acc2) Vec8<T>::load(y2 + pix * ld2 + off2 + c, v2);
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      v1[k] = acc1 ? v1[k] + vg[k] : vg[k];
+      v2[k] = acc2 ? v2[k] + vg[k] : vg[k];
+    }
+    Vec8<T>::store(y1 + pix * ld1 + off1 + c, v1);
+    Vec8<T>::store(y2 + pix * ld2 + off2 + c, v2);
+  }
+}
+
 }  // namespace yms
 
 using namespace yms;
@@ -581,6 +603,18 @@ yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, i
   YMS_DW_T(dtype, hipLaunchKernelGGL(add_views_kernel<TT>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, c / 8,
                                      (const TT*)a, a_ld, a_off, (const TT*)b, b_ld, b_off, (TT*)y, y_ld, y_off,
                                      accumulate));
+  return launch_status();
+}
+
+yms_status yms_add_grad2(int dtype, long npix, int c, const void* g, int g_ld, int g_off, void* y1, int ld1,
+                         int off1, int acc1, void* y2, int ld2, int off2, int acc2, void* stream) {
+  if (npix <= 0 || c <= 0 || c % 8 || !g || !y1 || !y2 || !dw_view_ok(g_ld, g_off, c) || !dw_view_ok(ld1, off1, c) ||
+      !dw_view_ok(ld2, off2, c))
+    return YMS_ERR_INVALID;
+  const long items = npix * (c / 8);
+  const unsigned grid = (unsigned)std::min<long>((items + 255) / 256, 16384);
+  YMS_DW_T(dtype, hipLaunchKernelGGL(add_grad2_kernel<TT>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, c / 8,
+                                     (const TT*)g, g_ld, g_off, (TT*)y1, ld1, off1, acc1, (TT*)y2, ld2, off2, acc2));
   return launch_status();
 }
 

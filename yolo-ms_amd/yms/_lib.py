@@ -95,6 +95,7 @@ _SIGS = {
     "yms_dwconv_wgrad_ws_bytes": (_SZ, [_DP]),
     "yms_dwconv_wgrad": (_I, [_DP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
     "yms_add_views": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P]),
+    "yms_add_grad2": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _I, _P, _I, _I, _I, _P]),
     "yms_map_match": (_I, [_I, _P, _P, _P, _P, _P, _P, _P, _P, _P, _P, _I, _P]),
     "yms_map_accumulate": (_I, [_I, _P, _P, _P, _P, _P, _I, _P, _P, _P]),
     "yms_det_loss_ws_bytes": (_SZ, [_I, _I, _I, _I]),

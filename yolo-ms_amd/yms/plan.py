@@ -509,6 +509,11 @@ class AddOp:
 
     def bwd(self, rt):
         y = self.y
+        if all(v is not None and acc is not None for v, acc in zip((self.a, self.b), self.acc)):
+            a, b = self.a, self.b
+            L.call("yms_add_grad2", rt.plan.dt, self.npix, self.c, rt.g(y), y.buf.ld, y.off, rt.g(a), a.buf.ld,
+                   a.off, self.acc[0], rt.g(b), b.buf.ld, b.off, self.acc[1], rt.st)
+            return
         for v, acc in zip((self.a, self.b), self.acc):
             if v is None or acc is None:
                 continue
