@@ -132,6 +132,10 @@ def conv_roofline(prof, label):
             # per-launch roofline of each layer's own arithmetic intensity, min(MFMA peak,
             # AI x HBM peak): sum over launches of max(flops / 2.5 PF, bytes / 8 TB/s) against the
             # measured time; bytes = input + output + weights once per launch (algorithmic)
+            "by_entry_point": {k.replace("yms_conv_", ""): {
+                "launches": v[0], "ms": round(v[1], 4), "tflops": round(v[2] / (v[1] * 1e-3) / 1e12, 1) if v[1] else 0.0,
+                "per_layer_roofline_frac": round(v[4] / v[1], 4) if v[1] else 0.0}
+                for k, v in prof.items() if k.startswith("yms_conv_") and v[2]},
             "per_layer_roofline": {
                 "t_attainable_ms": round(t_roof, 4), "t_measured_ms": round(ms, 4),
                 "frac": round(t_roof / ms, 4) if ms > 0 else 0.0,
