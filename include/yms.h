@@ -107,6 +107,16 @@ int yms_conv_stem_stats_rows(const yms_conv_shape* s);
 yms_status yms_conv_stem_fwd(const yms_conv_shape* s, const float* x, const float* w, void* y, int y_ld,
                              int y_off, const float* scale, const float* shift, int act, float* stats,
                              int stats_ld, void* stream);
+/* Stem weight gradient with the BN + SiLU backward apply fused in (the stem's dz has no other
+ * consumer: the input needs no gradient): dz = scale*(da - coef[c] - (z - mean)*invstd*coef[C+c]),
+ * da = gy * SiLU'(z*scale + shift) (act), rounded to s->dtype as the apply pass stores it; then
+ * dw[cout][cin][3][3] (+)= sum_pixels dz (x) im2col(x), x the NCHW fp32 input as in
+ * yms_conv_stem_fwd.  mean_invstd / coef as yms_bn_act_bwd_apply; ws >= yms_conv_stem_wgrad_ws_bytes. */
+size_t yms_conv_stem_wgrad_ws_bytes(const yms_conv_shape* s);
+yms_status yms_conv_stem_wgrad(const yms_conv_shape* s, const float* x, const void* gy, int gy_ld, int gy_off,
+                               const void* z, int z_ld, int z_off, const float* scale, const float* shift,
+                               const float* mean_invstd, const float* coef, int act, float* ws, size_t ws_bytes,
+                               float* dw, int accumulate, void* stream);
 /* dx (+)= conv_transpose(dz, W) with wpacked_t = yms_conv_pack_weight(.., for_dgrad=1). */
 yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
                           const void* wpacked_t, void* dx, int dx_ld, int dx_off,

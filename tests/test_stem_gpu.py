@@ -127,3 +127,44 @@ def test_model_stem_path_matches_generic_path(v, training, monkeypatch):
     for a, b in zip(outs["1"], outs["0"]):
         err = ((a - b).norm() / b.norm()).item()
         assert err < 2e-2, err
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("n,h,w,cout", [(2, 64, 64, 32), (3, 45, 78, 48), (1, 33, 20, 16)])
+def test_stem_wgrad_with_fused_bn_backward(dt, n, h, w, cout):
+    """yms_conv_stem_wgrad = BN+SiLU backward apply (bn_bwd_apply_kernel's dz, rounded to the
+    dtype) followed by the conv weight gradient against the NCHW input, vs fp64 torch."""
+    g = torch.Generator().manual_seed(n * 7 + h + cout)
+    x = torch.randn(n, 3, h, w, generator=g)
+    sh_ = shape(n, h, w, 3, cout, 3, 2, DT[dt])
+    sp = ctypes.pointer(sh_)
+    ho, wo = sh_.ho, sh_.wo
+    z = torch.randn(n, ho, wo, cout, generator=g).to(DT[dt])
+    gy = (torch.randn(n, ho, wo, cout, generator=g) * 0.1).to(DT[dt])
+    sc = torch.rand(cout, generator=g) + 0.5
+    sf = torch.randn(cout, generator=g) * 0.2
+    mu = torch.randn(cout, generator=g) * 0.1
+    istd = torch.rand(cout, generator=g) + 0.5
+    coef = torch.randn(2 * cout, generator=g) * 0.05
+    # reference dz exactly as bn_bwd_apply_kernel forms it (fp32), rounded to the dtype
+    zf, gf = z.float(), gy.float()
+    a = zf * sc + sf
+    s_ = torch.sigmoid(a)
+    da = gf * (s_ * (1 + a * (1 - s_)))
+    bz = -sc * coef[cout:] * istd
+    a0 = -sc * coef[:cout] - bz * mu
+    dz = (sc * da + a0 + bz * zf).to(DT[dt]).double()                   # [n, ho, wo, cout]
+    xr = x.to(DT[dt]).double()
+    ref = torch.nn.grad.conv2d_weight(xr, (cout, 3, 3, 3), dz.permute(0, 3, 1, 2), stride=2, padding=1)
+    ws = torch.empty(L.lib().yms_conv_stem_wgrad_ws_bytes(sp) // 4 + 1, device="cuda")
+    dw = torch.full((cout, 3, 3, 3), float("nan"), device="cuda")
+    xd, zd, gd = x.cuda(), z.cuda(), gy.cuda()
+    mi = torch.cat([mu, istd]).cuda()
+    scd, sfd, cd = sc.cuda(), sf.cuda(), coef.cuda()
+    L.call("yms_conv_stem_wgrad", sp, xd.data_ptr(), gd.data_ptr(), cout, 0, zd.data_ptr(), cout, 0, scd.data_ptr(),
+           sfd.data_ptr(), mi.data_ptr(), cd.data_ptr(), L.ACT_SILU, ws.data_ptr(), ws.numel() * 4, dw.data_ptr(), 0,
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    out = dw.double().cpu()
+    rel = ((out - ref).norm() / ref.norm()).item()
+    assert rel < 2e-3, rel

@@ -401,21 +401,34 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
   }
 }
 
-// dw[c][t] (+)= sum_b ws[b][t][c]: 64 outputs per block, wave w sums blocks b = w (mod 4) in order,
-// the four partials are added in a fixed order
-__global__ __launch_bounds__(256) void dwconv_wgrad_reduce_kernel(const float* ws, int blocks, int C, int KK, float* dw,
-                                                                  int accumulate) {
-  __shared__ float red[4][64];
+// dw[c][t] (+)= sum_b ws[b][t][c]: 64 outputs per block, 16 waves; wave w sums blocks
+// b = w (mod 16) into 4 independent partials (4 loads in flight per lane; one dependent chain
+// over ~500 rows made the reduce latency-bound), then a fixed-order tree over the waves
+__global__ __launch_bounds__(1024) void dwconv_wgrad_reduce_kernel(const float* ws, int blocks, int C, int KK, float* dw,
+                                                                   int accumulate) {
+  __shared__ float red[16][64];
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int j = blockIdx.x * 64 + lane;
   const long stride = (long)C * KK;
-  float s = 0.f;
-  if (j < stride)
-    for (int b = w; b < blocks; b += 4) s += ws[(long)b * stride + j];
-  red[w][lane] = s;
+  float s0 = 0.f, s1 = 0.f, s2 = 0.f, s3 = 0.f;
+  if (j < stride) {
+    int b = w;
+    for (; b + 48 < blocks; b += 64) {
+      s0 += ws[(long)b * stride + j];
+      s1 += ws[(long)(b + 16) * stride + j];
+      s2 += ws[(long)(b + 32) * stride + j];
+      s3 += ws[(long)(b + 48) * stride + j];
+    }
+    for (; b < blocks; b += 16) s0 += ws[(long)b * stride + j];
+  }
+  red[w][lane] = (s0 + s1) + (s2 + s3);
   __syncthreads();
+  for (int h = 8; h >= 1; h >>= 1) {
+    if (w < h) red[w][lane] += red[w + h][lane];
+    __syncthreads();
+  }
   if (w == 0 && j < stride) {
-    s = ((red[0][lane] + red[1][lane]) + red[2][lane]) + red[3][lane];
+    const float s = red[0][lane];
     const int t = j / C, c = j - t * C;
     float* o = dw + (long)c * KK + t;
     *o = accumulate ? *o + s : s;
@@ -588,7 +601,7 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
   const int KK2 = s->k * s->k;
-  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(256), 0, st, ws,
+  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
                      blocks, s->c, KK2, dw, accumulate);
   return launch_status();
 }

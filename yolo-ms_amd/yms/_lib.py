@@ -64,6 +64,8 @@ _SIGS = {
     "yms_conv_stem_supported": (_I, [_SP]),
     "yms_conv_stem_stats_rows": (_I, [_SP]),
     "yms_conv_stem_fwd": (_I, [_SP, _P, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
+    "yms_conv_stem_wgrad_ws_bytes": (_SZ, [_SP]),
+    "yms_conv_stem_wgrad": (_I, [_SP, _P, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _I, _P, _SZ, _P, _I, _P]),
     "yms_conv_dgrad": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
     "yms_conv_wgrad_ws_bytes": (_SZ, [_SP]),
     "yms_conv_wgrad": (_I, [_SP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),

@@ -228,6 +228,8 @@ class ConvOp:
             plan.need_scratch("coef", 8 * c)
             self.cnt = plan.counter()
             plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
+            if self.stem_input is not None:
+                plan.need_scratch("wgrad", L.lib().yms_conv_stem_wgrad_ws_bytes(self.sp))
 
     def pack_specs(self):
         """(shape, fp32 weight, arena byte offset of the packed copy, for_dgrad) per training pack."""
@@ -300,6 +302,19 @@ class ConvOp:
                    base + self.sh, base + self.mi, self.act, ws, rt.st)
             L.call("yms_bn_act_bwd_finalize", c, ws, L.lib().yms_bn_bwd_rows(self.npix, c), self.npix,
                    rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        if self.stem_input is not None:
+            # the stem's input needs no gradient: the apply pass is fused into the weight
+            # gradient, which reads gy, z and the NCHW input on the side stream
+            dw = rt.pgrad(self.pw)
+            if dw is not None:
+                st = rt.wst()
+                xs = rt.stem_x[self.stem_input]
+                if rt.side is not None:
+                    xs.record_stream(rt.side)
+                L.call("yms_conv_stem_wgrad", self.sp, xs.data_ptr(), gy, gyl, gyo, z, self.zld, 0, base + self.sc,
+                       base + self.sh, base + self.mi, coef, self.act, rt.gbase + rt.plan.gscratch["wgrad"],
+                       L.lib().yms_conv_stem_wgrad_ws_bytes(self.sp), dw, 0, st)
+            return
         gres = rt.g(r) if r is not None else None
         gro = (r.buf.ld, r.off) if r is not None else (0, 0)
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
@@ -697,9 +712,9 @@ class Plan:
 
     def _find_stems(self):
         """Inputs whose only reader is a stem-shaped Conv (3x3 stride 2 over <= 3 channels, no
-        residual, 16-bit compute): that conv reads the NCHW fp32 input itself
-        (yms_conv_stem_fwd); eval then skips the NHWC input pack (training keeps it for the
-        conv's weight gradient).  YMS_STEM=0 keeps the generic pack + implicit-GEMM path."""
+        residual, 16-bit compute, input without gradient): that conv reads the NCHW fp32 input
+        itself (yms_conv_stem_fwd, and yms_conv_stem_wgrad with the BN backward apply fused in),
+        so the NHWC input pack goes.  YMS_STEM=0 keeps the generic pack + implicit-GEMM path."""
         out = {}
         if self.dt == L.F32 or os.environ.get("YMS_STEM", "1") == "0":
             return out
@@ -710,6 +725,7 @@ class Plan:
                 continue
             op = readers[0]
             if (op.x.buf is v.buf and op.x.off == 0 and op.x.c == v.c and op.res is None and v.buf.ld == r8(v.c)
+                    and not v.buf.needs_grad
                     and L.lib().yms_conv_stem_supported(op.sp)):
                 op.stem_input = i
                 out[i] = op

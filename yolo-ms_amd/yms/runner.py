@@ -64,21 +64,14 @@ def get_plan(module, inputs, dt, training):
     return plan
 
 
-def _load_inputs(plan, rt, inputs, side=None):
+def _load_inputs(plan, rt, inputs):
     for i, (x, v) in enumerate(zip(inputs, plan.inputs)):
         xc = x.contiguous()
         st = rt.st
         if i in plan.stem_inputs:
-            # the stem conv reads the NCHW input itself; only training's weight gradient needs
-            # the packed NHWC copy, which is then packed on the weight-gradient side stream (off
-            # the forward's critical path; the stem's wgrad runs on that stream, after it)
+            # the stem conv reads the NCHW input itself, forward and weight gradient: no pack
             rt.stem_x[i] = xc if xc.dtype == torch.float32 else xc.float()
-            if not plan.training:
-                continue
-            if side is not None:
-                side.wait_stream(torch.cuda.current_stream(xc.device))
-                xc.record_stream(side)
-                st = side.cuda_stream
+            continue
         if v.off == 0 and xc.dtype == torch.float32:
             L.call("yms_pack_input", plan.dt, xc.shape[0], xc.shape[1], xc.shape[2], xc.shape[3], xc.data_ptr(),
                    rt.a(v), v.buf.ld, st)
@@ -162,10 +155,7 @@ class _PlanFn(torch.autograd.Function):
         stream = L.stream_ptr(dev)
         arena = plan.new_arena(dev, stream)
         rt = Rt(plan, arena.data_ptr(), stream, True)
-        side = _side_stream(dev) if (WGRAD_SIDE_STREAM and plan.stem_inputs) else None
-        if side is not None:
-            arena.record_stream(side)      # a forward without backward must not recycle it early
-        _load_inputs(plan, rt, inputs, side)
+        _load_inputs(plan, rt, inputs)
         plan.prepack(rt)
         for op in plan.ops:
             op.fwd(rt)
