@@ -262,6 +262,19 @@ def cpu_baseline_infer(version, nc, size, batch=8, steps=12):
             f"({dt:.1f} s), torch threads={threads}"}
 
 
+def make_sgd(params):
+    """The reference's SGD-nesterov step (train.py optimizer settings); one fused multi-tensor
+    kernel where torch has it for this device (YMS_SGD=foreach forces the foreach kernels)."""
+    kw = dict(lr=0.01, momentum=0.937, nesterov=True, weight_decay=5e-4)
+    params = list(params)
+    if os.environ.get("YMS_SGD", "fused") == "fused":
+        try:
+            return torch.optim.SGD(params, fused=True, **kw)
+        except (RuntimeError, TypeError, ValueError):
+            pass
+    return torch.optim.SGD(params, foreach=True, **kw)
+
+
 def measure_ms_family(a, dev, dtype):
     """The MS-Block / HKS graph of the same size class (the reference holds it only as
     a diagram, so these lines are not oracle-pinned like configs[2]): training step with the GPU
@@ -279,8 +292,7 @@ def measure_ms_family(a, dev, dtype):
     set_compute_dtype(m, dtype)
     if a.mode in ("both", "train"):
         m.train()
-        opt = torch.optim.SGD(m.parameters(), lr=0.01, momentum=0.937, nesterov=True, weight_decay=5e-4,
-                              foreach=True)
+        opt = make_sgd(m.parameters())
         x = torch.randn(a.batch, 3, a.size, a.size, device=dev, generator=torch.Generator(device=dev).manual_seed(7))
         crit = ComputeLoss(m.head, a.nc, dev, (a.size, a.size))
         tg = synth_targets(a.batch, a.nc, a.gts, 4321, dev)
@@ -356,8 +368,7 @@ def main():
     # ---------------- training (configs[2]) ----------------
     if a.mode in ("both", "train"):
         model.train()
-        opt = torch.optim.SGD(model.parameters(), lr=0.01, momentum=0.937, nesterov=True, weight_decay=5e-4,
-                              foreach=True)
+        opt = make_sgd(model.parameters())
         g = torch.Generator(device=dev).manual_seed(1234 + rank)
         x = torch.randn(a.batch, 3, a.size, a.size, device=dev, generator=g)
         if a.loss == "compute":

@@ -47,3 +47,10 @@ for q, rs in sorted(byq.items(), key=lambda kv: -len(kv[1])):
           f"(n={len(gaps)}, >20us: {sum(g for g in gaps if g > 20000) / 1e6:.3f} ms)")
     for k, v in fams.most_common(14):
         print(f"   {v / 1e6:8.3f} ms  {k}")
+
+# tail of the step: the last kernels per queue (relative ms) -- is the side stream backlogged
+# when the main stream's backward ends?
+print("last 24 kernels of the step (queue, start..end ms, name):")
+for r in step[-24:]:
+    s, e = (int(r["Start_Timestamp"]) - t0) / 1e6, (int(r["End_Timestamp"]) - t0) / 1e6
+    print(f"  q{r['Queue_Id']:>3} {s:8.3f}..{e:8.3f}  {fam(r['Kernel_Name'])}")
