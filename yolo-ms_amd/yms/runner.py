@@ -156,8 +156,23 @@ class _PlanFn(torch.autograd.Function):
         arena = plan.new_arena(dev, stream)
         rt = Rt(plan, arena.data_ptr(), stream, True)
         _load_inputs(plan, rt, inputs)
-        plan.prepack(rt)
-        for op in plan.ops:
+        ops = plan.ops
+        if (WGRAD_SIDE_STREAM and os.environ.get("YMS_PACK_SIDE", "1") != "0" and plan.ops
+                and plan.ops[0] in plan.stem_inputs.values()):
+            # the stem conv reads the fp32 weight itself: the step's weight packs go to the side
+            # stream and overlap it; every later conv is ordered after them
+            main, side = torch.cuda.current_stream(dev), _side_stream(dev)
+            side.wait_stream(main)
+            arena.record_stream(side)
+            rt.st = side.cuda_stream
+            plan.prepack(rt)
+            rt.st = stream
+            ops[0].fwd(rt)
+            main.wait_stream(side)
+            ops = ops[1:]
+        else:
+            plan.prepack(rt)
+        for op in ops:
             op.fwd(rt)
         state.arena = arena
         state.rt = rt
