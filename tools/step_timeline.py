@@ -54,3 +54,17 @@ print("last 24 kernels of the step (queue, start..end ms, name):")
 for r in step[-24:]:
     s, e = (int(r["Start_Timestamp"]) - t0) / 1e6, (int(r["End_Timestamp"]) - t0) / 1e6
     print(f"  q{r['Queue_Id']:>3} {s:8.3f}..{e:8.3f}  {fam(r['Kernel_Name'])}")
+
+# the largest idle gaps of the busiest queue, with the kernels around them
+q1 = sorted(byq.items(), key=lambda kv: -len(kv[1]))[0][1]
+gl = []
+end, prev = int(q1[0]["Start_Timestamp"]), None
+for r in q1:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    if s > end:
+        gl.append((s - end, (end - t0) / 1e6, fam(prev["Kernel_Name"]) if prev else "", fam(r["Kernel_Name"])))
+    if e > end:
+        end, prev = e, r
+print("largest idle gaps on the main queue (us, at ms, after -> before):")
+for g, at, a, b in sorted(gl, reverse=True)[:25]:
+    print(f"  {g / 1e3:7.1f} us @ {at:7.3f}  {a} -> {b}")
