@@ -195,3 +195,35 @@ def test_big_segment_grid_edge_cases():
     p[0, 77, 1] = np.inf
     _check(p, 0.25, 0.5)
     _check(seg(8, 40), 0.25, -0.5)
+
+
+def test_nms_on_side_stream_overlapping_next_forward():
+    """The serving pipeline of bench.py (--nms-overlap): batch k's NMS on a second stream while
+    batch k+1's forward runs on the main stream gives the same keep lists as one stream."""
+    from yms import set_compute_dtype
+    from yolov8.yolov8 import YOLOv8
+
+    torch.manual_seed(0)
+    m = YOLOv8("n", 80).cuda().eval()
+    m.head.stride = torch.tensor([8.0, 16.0, 32.0])
+    set_compute_dtype(m, torch.bfloat16)
+    xs = [torch.randn(2, 3, 128, 128, device="cuda", generator=torch.Generator(device="cuda").manual_seed(s))
+          for s in range(3)]
+    ref = []
+    for x in xs:
+        _, _, keep, klbl, cnt = ops.batched_nms_indices(m(x), 0.25, 0.45)
+        ref.append((keep.clone(), klbl.clone(), cnt.clone()))
+    side = torch.cuda.Stream()
+    got = []
+    for x in xs:
+        y = m(x)
+        side.wait_stream(torch.cuda.current_stream())
+        y.record_stream(side)
+        with torch.cuda.stream(side):
+            got.append(ops.batched_nms_indices(y, 0.25, 0.45)[2:])
+    torch.cuda.synchronize()
+    for (k0, l0, c0), (k1, l1, c1) in zip(ref, got):
+        assert torch.equal(c0, c1)
+        for b in range(c0.numel()):
+            n = int(c0[b])
+            assert torch.equal(k0[b, :n], k1[b, :n]) and torch.equal(l0[b, :n], l1[b, :n])
