@@ -153,6 +153,7 @@ class Rt:
         self.eval_base = None    # eval cache base pointer (packed weights + folded BN)
         self.prepacked = False   # training: all weight packs already issued (Plan.prepack)
         self.stem_x = {}         # plan input index -> NCHW fp32 tensor read by a stem ConvOp
+        self._ev = None          # wst(): main -> side ordering event
         self.main = None         # backward: torch stream objects (main, weight-gradient side stream)
         self.side = None
 
@@ -174,7 +175,11 @@ class Rt:
         "wgrad" scratch stays in stream order."""
         if self.side is None:
             return self.st
-        self.side.wait_stream(self.main)
+        # one reusable event (a wait binds the record made before it), not a new one per layer
+        if self._ev is None:
+            self._ev = torch.cuda.Event()
+        self._ev.record(self.main)
+        self.side.wait_event(self._ev)
         return self.side.cuda_stream
 
 
@@ -224,12 +229,15 @@ class ConvOp:
                 self.stats_rows = L.lib().yms_conv_stats_rows(self.sp)
             self.stats_ld = L.lib().yms_conv_stats_ld(self.sp)
             plan.need_scratch("stats", 4 * self.stats_rows * (2 * self.stats_ld + 1))
-            plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
+            self.bwd_rows = L.lib().yms_bn_bwd_rows(self.npix, c)
+            plan.need_scratch("bwd", 4 * 2 * c * self.bwd_rows)
             plan.need_scratch("coef", 8 * c)
             self.cnt = plan.counter()
-            plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
+            self.wg_ws = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
+            plan.need_scratch("wgrad", self.wg_ws)
             if self.stem_input is not None:
-                plan.need_scratch("wgrad", L.lib().yms_conv_stem_wgrad_ws_bytes(self.sp))
+                self.wg_ws = L.lib().yms_conv_stem_wgrad_ws_bytes(self.sp)
+                plan.need_scratch("wgrad", self.wg_ws)
 
     def pack_specs(self):
         """(shape, fp32 weight, arena byte offset of the packed copy, for_dgrad) per training pack."""
@@ -300,7 +308,7 @@ class ConvOp:
         else:
             L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
                    base + self.sh, base + self.mi, self.act, ws, rt.st)
-            L.call("yms_bn_act_bwd_finalize", c, ws, L.lib().yms_bn_bwd_rows(self.npix, c), self.npix,
+            L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix,
                    rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
         if self.stem_input is not None:
             # the stem's input needs no gradient: the apply pass is fused into the weight
@@ -314,7 +322,7 @@ class ConvOp:
                 xs = rt.stem_x[self.stem_input]
                 L.call("yms_conv_stem_wgrad", self.sp, xs.data_ptr(), gy, gyl, gyo, z, self.zld, 0, base + self.sc,
                        base + self.sh, base + self.mi, coef, self.act, rt.gbase + rt.plan.gscratch["wgrad"],
-                       L.lib().yms_conv_stem_wgrad_ws_bytes(self.sp), dw, 0, st)
+                       self.wg_ws, dw, 0, st)
             return
         gres = rt.g(r) if r is not None else None
         gro = (r.buf.ld, r.off) if r is not None else (0, 0)
@@ -326,7 +334,7 @@ class ConvOp:
                    self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
-            wsz = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
+            wsz = self.wg_ws
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
                    rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
 
