@@ -236,8 +236,10 @@ class ConvOp:
             self.wg_ws = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
             plan.need_scratch("wgrad", self.wg_ws)
             if self.stem_input is not None:
+                # its own scratch: the stem's wgrad runs on the MAIN stream while the side stream
+                # may still be in the previous layers' wgrads, which share the "wgrad" scratch
                 self.wg_ws = L.lib().yms_conv_stem_wgrad_ws_bytes(self.sp)
-                plan.need_scratch("wgrad", self.wg_ws)
+                plan.need_scratch("stemwg", self.wg_ws)
 
     def pack_specs(self):
         """(shape, fp32 weight, arena byte offset of the packed copy, for_dgrad) per training pack."""
@@ -312,7 +314,7 @@ class ConvOp:
                    rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
         if self.stem_input is not None:
             # the stem's input needs no gradient: the apply pass is fused into the weight
-            # gradient, which reads gy, z and the NCHW input on the side stream
+            # gradient, which reads gy, z and the NCHW input.
             # It runs on the MAIN stream: the stem is the backward's last layer, so the main stream
             # is idle from here on while the side stream still drains the previous layers'
             # weight gradients -- the two then overlap instead of queueing (step tail 0.53 ms).
@@ -321,7 +323,8 @@ class ConvOp:
                 st = rt.st if os.environ.get("YMS_STEM_WG_SIDE", "0") == "0" else rt.wst()
                 xs = rt.stem_x[self.stem_input]
                 L.call("yms_conv_stem_wgrad", self.sp, xs.data_ptr(), gy, gyl, gyo, z, self.zld, 0, base + self.sc,
-                       base + self.sh, base + self.mi, coef, self.act, rt.gbase + rt.plan.gscratch["wgrad"],
+                       base + self.sh, base + self.mi, coef, self.act,
+                       rt.gbase + rt.plan.gscratch["stemwg"],
                        self.wg_ws, dw, 0, st)
             return
         gres = rt.g(r) if r is not None else None
@@ -694,7 +697,7 @@ class Plan:
         # grad arena: activation grads share the activation layout, then backward scratch
         Lg = Layout()
         Lg.size = self.act_bytes
-        self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf")}
+        self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf", "stemwg")}
         self.gscratch["cnt"] = Lg.alloc(16 * max(self.n_counters, 1))
         self.garena_bytes = Lg.size
         self.eval_bytes = Le.size
@@ -775,11 +778,9 @@ class Plan:
             self._eval_sig = sig
         return self._eval_arena.data_ptr()
 
-    def prepack(self, rt):
-        """Training: issue every conv weight pack of the step -- one batched launch for the
-        plain packs (device job table of arena OFFSETS, cached per parameter set, so it is valid
-        for any arena and is built before any graph capture) plus the stride-2 dgrad parity
-        packs individually."""
+    def pack_table(self):
+        """The batched pack's device job table (built and uploaded on the CURRENT stream on a
+        cache miss: call it before handing prepack to another stream)."""
         specs = [sp for op in self.ops if hasattr(op, "pack_specs") for sp in op.pack_specs()]
         key = tuple((w, dst) for _, w, dst, _ in specs)
         cache = self.__dict__.setdefault("_pack_tables", {})
@@ -799,7 +800,14 @@ class Plan:
             if len(cache) >= 4:
                 cache.clear()
             ent = cache[key] = (table, len(jobs), singles)
-        table, nj, singles = ent
+        return ent
+
+    def prepack(self, rt, ent=None):
+        """Training: issue every conv weight pack of the step on rt.st -- one batched launch for
+        the plain packs (device job table of arena OFFSETS, cached per parameter set, so it is
+        valid for any arena and is built before any graph capture) plus the stride-2 dgrad
+        parity packs individually."""
+        table, nj, singles = ent if ent is not None else self.pack_table()
         L.call("yms_conv_pack_weights_batched", nj, table.data_ptr(), rt.base, rt.st)
         for sp, w, dst, fd in singles:
             L.call("yms_conv_pack_weight", sp, w, rt.base + dst, fd, rt.st)

@@ -162,10 +162,12 @@ class _PlanFn(torch.autograd.Function):
             # the stem conv reads the fp32 weight itself: the step's weight packs go to the side
             # stream and overlap it; every later conv is ordered after them
             main, side = torch.cuda.current_stream(dev), _side_stream(dev)
+            ent = plan.pack_table()          # a first-call table upload goes on main, before the wait
             side.wait_stream(main)
             arena.record_stream(side)
             rt.st = side.cuda_stream
-            plan.prepack(rt)
+            plan.prepack(rt, ent)
+            ent[0].record_stream(side)       # the table may be evicted from the plan's cache later
             rt.st = stream
             ops[0].fwd(rt)
             main.wait_stream(side)
