@@ -164,12 +164,14 @@ class _PlanFn(torch.autograd.Function):
             main, side = torch.cuda.current_stream(dev), _side_stream(dev)
             ent = plan.pack_table()          # a first-call table upload goes on main, before the wait
             side.wait_stream(main)
-            arena.record_stream(side)
             rt.st = side.cuda_stream
             plan.prepack(rt, ent)
-            ent[0].record_stream(side)       # the table may be evicted from the plan's cache later
             rt.st = stream
             ops[0].fwd(rt)
+            # main joins the side stream right here, so any later reuse of the arena's or the
+            # table's memory (main-stream ordered) comes after the packs: no record_stream (which
+            # would defer the arena's reuse and, with the host steps ahead, make the caching
+            # allocator map a second ~100 GB arena for YOLO-MS-L)
             main.wait_stream(side)
             ops = ops[1:]
         else:
