@@ -18,10 +18,13 @@ Follows yolov8/tools/loss.py (rafaelghiorzi/YOLO-MS) line by line in semantics:
     weights (1 - frac, frac), indices clamped to [0, 15], mean over foreground x 4 (NaN -> 0);
     without foreground: the BCE mean once.  Each term / batch, total = 7.5 box + 0.5 cls + 1.5 dfl.
 
-Parity for this file is UNPINNED: the reference module imports torchvision (loss.py:4, unused
-names) which is not installed here, so it cannot be imported to produce golden vectors, and its
-own test (loss.py:680-771) only checks that the loss is finite.  Top-k ties are broken towards the
-lower anchor index (torch.topk's order for equal values is unspecified; continuous IoUs do not tie).
+Parity is PINNED: tests/golden/make_loss_golden.py runs the reference's own ComputeLoss in the build
+container (its unused torchvision imports at loss.py:4 resolve to a stub module whose functions raise
+if called) and tests/test_loss_golden.py requires this restatement to reproduce those fixtures
+bit-for-bit in fp32 (values and every gradient element): all four IoU types, images without GT, a GT
+without foreground, shared anchors, pos_weight, bf16-rounded maps, the 640 grid at nc = 80.  Top-k
+ties are broken towards the lower anchor index (torch.topk's order for equal values is unspecified;
+continuous IoUs do not tie).
 Only tests/ may import this module.
 """
 from __future__ import annotations

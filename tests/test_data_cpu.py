@@ -78,3 +78,25 @@ def test_resize_reference_known_answers():
     # flips act before the resize
     fl = P.resize_normalize(g, 4, 4, (0, 0, 0), (1, 1, 1), flags=1)[0] * 255
     assert np.allclose(fl[0], row0[::-1], atol=1e-4)
+
+
+def test_flip_streams_differ_across_workers_and_epochs(tmp_path):
+    """Each DataLoader worker (and each epoch of non-persistent workers) draws its own flip stream:
+    a Generator built in __init__ would be forked identically into every worker."""
+    ann = _coco(tmp_path, [(8, 8)] * 2)
+    ds = D.COCODetection(str(tmp_path), str(ann), img_size=(8, 8), num_classes=2, fliplr=0.5, flipud=0.5)
+    idx = [0, 1] * 32
+    sub = torch.utils.data.Subset(ds, idx)
+
+    def epoch(seed):
+        torch.manual_seed(seed)
+        dl = torch.utils.data.DataLoader(sub, batch_size=16, num_workers=2, collate_fn=ds.collate_fn,
+                                         multiprocessing_context="fork")
+        return [tuple(f) for _, f, _ in dl]
+
+    e1 = epoch(0)
+    assert len(e1) == 4
+    # batches 0 and 2 come from worker 0, 1 and 3 from worker 1: same indices, different draws
+    assert e1[0] != e1[1] and e1[2] != e1[3]
+    assert epoch(1) != e1                    # a new epoch (new base seed) draws anew
+    assert epoch(0) == e1                    # and the stream is reproducible from torch's seed

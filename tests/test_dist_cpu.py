@@ -86,7 +86,13 @@ def _worker(rank, world, port, q):
             m.running_mean.fill_(5.0 * (rank + 1))
         dp.train()
         dp(torch.zeros(2, 4, 3, 3))                   # buffers re-synced before forward
-        q.put((rank, ok_grad, launched, ok_bcast, m.running_mean[0].item()))
+        rm1 = m.running_mean[0].item()
+        # a cast after wrapping replaces the buffers: the broadcast must follow the new tensors
+        m.double()
+        with torch.no_grad():
+            m.running_mean.fill_(7.0 * (rank + 1))
+        dp(torch.zeros(2, 4, 3, 3, dtype=torch.float64))
+        q.put((rank, ok_grad, launched, ok_bcast, (rm1, m.running_mean[0].item())))
     finally:
         dist.destroy_process_group()
 
@@ -107,7 +113,8 @@ def test_bucketed_allreduce_gloo_world2():
         assert launched[0] == launched[1] >= 3, launched
         assert ok_bcast, rank
         # rank 0's buffer (5.0) broadcast before forward, then BN2d(momentum 0.1) on zeros
-        assert abs(rm - 0.9 * 5.0) < 1e-5, rm
+        assert abs(rm[0] - 0.9 * 5.0) < 1e-5, rm
+        assert abs(rm[1] - 0.9 * 7.0) < 1e-5, rm     # rank 0's value after .double()
 
 
 def test_bucket_layout_on_the_real_plan():

@@ -1,6 +1,6 @@
 """Known-answer tests of the ComputeLoss restatement (oracle/loss_ref.py; yolov8/tools/loss.py:9-677).
-Parity of the restatement is unpinned (the reference module imports torchvision, absent here), so
-these pin the semantics it claims on hand-computed cases."""
+The restatement is pinned to the reference's own outputs by tests/test_loss_golden.py; these add
+hand-computed known answers for the semantics it claims."""
 import math
 
 import torch

@@ -3,12 +3,17 @@ restatement of the reference's ComputeLoss (oracle/loss_ref.py; loss.py:94-677):
 and d(total)/d(head maps) (autograd through the restatement), on random head maps with targets
 covering the reference's edge cases -- images without GT, a GT no prediction overlaps (no
 foreground), GTs of different classes sharing anchors (overwritten boxes, accumulated class bits),
-every IoU variant, BCE pos_weight, bf16 maps, the full 640x640 anchor grid at nc = 80.  Parity of
-the restatement itself is unpinned (the reference module cannot be imported here)."""
+every IoU variant, BCE pos_weight, bf16 maps, the full 640x640 anchor grid at nc = 80.  The
+restatement is pinned bit-for-bit to the reference's own ComputeLoss by the fixtures of
+tests/golden/make_loss_golden.py (tests/test_loss_golden.py); test_loss_vs_reference_fixtures checks
+the GPU kernels against those fixtures directly."""
+import numpy as np
 import pytest
 import torch
 
+import vectors as V
 from oracle import loss_ref as R
+from test_loss_golden import CASES, check_against_fixture
 from yolov8.tools.loss import ComputeLoss, det_loss
 
 pytestmark = pytest.mark.gpu
@@ -58,6 +63,24 @@ def _check(preds_cpu, targets, nc, img, strides, dtype=torch.float32, iou_type="
         rel = ((gg - r.grad).norm() / r.grad.norm().clamp_min(1e-30)).item()
         assert rel < gtol, rel
     return o
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_loss_vs_reference_fixtures(name):
+    """det_loss vs the reference ComputeLoss's own outputs (fp32 maps; bf16 for the bf16-rounded case,
+    whose gradient is stored in bf16: half-ulp 2^-9 relative per element)."""
+    z = V.load_loss_case(name)
+    bf16 = bool(z["bf16"][0])
+    dtype = torch.bfloat16 if bf16 else torch.float32
+    vtol, gtol = (1e-4, 4e-3) if bf16 else (2e-5, 2e-4)
+    for iou in z["ious"]:
+        preds = [_channels_last(torch.from_numpy(m), dtype).requires_grad_(True) for m in z["maps"]]
+        pw = None if "pos_weight" not in z else torch.from_numpy(z["pos_weight"])
+        out, grads = det_loss(preds, torch.from_numpy(z["targets"]).to(DEV), z["nc"], z["img"],
+                              iou_type=iou, pos_weight=pw)
+        vals = out.cpu().double().numpy()
+        assert np.isfinite(vals).all()
+        check_against_fixture(z, iou, vals, [g.float().cpu().double().numpy() for g in grads], vtol, gtol)
 
 
 @pytest.mark.parametrize("iou_type", ["ciou", "giou", "diou", "iou"])
@@ -112,3 +135,18 @@ def test_compute_loss_module_backward_through_model():
     grads = [p.grad for p in m.parameters() if p.requires_grad]
     assert all(g is not None and torch.isfinite(g).all() for g in grads)
     assert sum(float(g.abs().sum()) > 0 for g in grads) >= len(grads) - 1   # DFL projection excluded
+
+
+def test_loss_terms_are_reported_not_differentiable():
+    """loss_tensor -> (total, terms): total carries d(total)/d(maps); the terms are values, and a
+    backward through one of them raises instead of being dropped silently."""
+    B, nc = 2, 7
+    preds = [_channels_last(p, torch.float32).requires_grad_(True)
+             for p in _maps(B, nc, [(8, 8), (4, 4), (2, 2)], 3)]
+    crit = ComputeLoss(None, nc, DEV, (64, 64))
+    total, terms = crit.loss_tensor(preds, _targets(B, nc, 4, 5).to(DEV))
+    assert terms.shape == (3,) and not terms.requires_grad
+    with pytest.raises(RuntimeError):
+        terms[0].backward()
+    total.backward()
+    assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in preds)

@@ -120,7 +120,8 @@ class COCODetection(torch.utils.data.Dataset):
         self.img_h, self.img_w = img_size
         self.num_classes = num_classes
         self.fliplr, self.flipud = fliplr, flipud
-        self.rng = np.random.default_rng(seed)
+        self.seed = int(seed)
+        self._draws = 0
         d = json.load(open(annotations_file))
         self.imgs = {im["id"]: im for im in d.get("images", [])}
         self.img_to_anns = defaultdict(list)
@@ -158,11 +159,23 @@ class COCODetection(torch.utils.data.Dataset):
         boxes, labels = self.annotations(idx)
         h0, w0 = image.shape[:2]
         t = coco_boxes_to_targets(boxes, labels, w0, h0, self.img_w, self.img_h)
-        flags = (int(self.rng.random() < self.fliplr) if self.fliplr > 0 else 0) | \
-                ((int(self.rng.random() < self.flipud) << 1) if self.flipud > 0 else 0)
+        rng = self.sample_rng(idx)
+        flags = (int(rng.random() < self.fliplr) if self.fliplr > 0 else 0) | \
+                ((int(rng.random() < self.flipud) << 1) if self.flipud > 0 else 0)
         if flags:
             t = flip_targets(t, flags)
         return image, t, flags
+
+    def sample_rng(self, idx):
+        """Generator for one sample's random draws, seeded from (dataset seed, process stream, idx,
+        draw count).  In a DataLoader worker the stream is torch's per-worker seed (base seed drawn
+        anew for every epoch's iterator + worker id), so workers and epochs draw different streams;
+        in the main process it is torch.initial_seed() and the draw counter moves epochs apart.  A
+        Generator created once in __init__ would be forked unchanged into every worker instead."""
+        info = torch.utils.data.get_worker_info()
+        stream = info.seed if info is not None else torch.initial_seed()
+        self._draws += 1
+        return np.random.default_rng([self.seed, stream & 0xFFFFFFFFFFFFFFFF, int(idx), self._draws])
 
     def collate_fn(self, batch):
         """Host half of the collate: images stay decoded uint8; targets -> [M, 6] (dataset.py:235-267)."""

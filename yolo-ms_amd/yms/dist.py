@@ -137,12 +137,22 @@ class DataParallel(nn.Module):
             return
         flat = torch._utils._flatten_dense_tensors([b for _, _, b in mods])
         off = 0
+        self._views = []
         for m, n, b in mods:
             m._buffers[n] = flat[off:off + b.numel()].view_as(b)
+            self._views.append((m, n, m._buffers[n].data_ptr()))
             off += b.numel()
         self._flat = flat
 
+    def _flat_is_current(self):
+        """True while every buffer is still the view of ``_flat`` it was made: ``.to()``, ``.half()``
+        or ``load_state_dict(assign=True)`` on the wrapped module replace buffers, and a broadcast of
+        the stale flat tensor would then leave the ranks' BN statistics silently diverged."""
+        return all(m._buffers.get(n) is not None and m._buffers[n].data_ptr() == p for m, n, p in self._views)
+
     def _sync_buffers(self):
+        if self._flat is not None and not self._flat_is_current():
+            self._flat_buffers()
         if self._flat is not None:
             dist.broadcast(self._flat, 0, group=self.group)
             return

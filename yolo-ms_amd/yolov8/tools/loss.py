@@ -132,21 +132,25 @@ def det_loss(preds, targets, nc, img_size, strides=(8.0, 16.0, 32.0), iou_type="
 
 
 class _DetLossFn(torch.autograd.Function):
+    """-> (total [], terms [3] = box, cls, dfl).  The kernel produces d(total)/d(maps) only, so the
+    terms are marked non-differentiable: backward through one of them raises instead of dropping it
+    (the reference returns the terms as floats, loss.py:666-672)."""
+
     @staticmethod
     def forward(ctx, cfg, targets, *preds):
         out, grads = det_loss(list(preds), targets, *cfg, need_grad=any(p.requires_grad for p in preds))
         ctx.grads = grads
         ctx.n_preds = len(preds)
-        return out
+        terms = out[1:].clone()
+        ctx.mark_non_differentiable(terms)
+        return out[0].clone(), terms
 
     @staticmethod
-    def backward(ctx, gout):
+    def backward(ctx, g, _gterms):
         grads = ctx.grads
         ctx.grads = None
         if grads is None:
             return (None, None) + (None,) * ctx.n_preds
-        # only the total carries the fused gradient; the per-term outputs are reported values
-        g = gout[0]
         return (None, None, *[gr * g.to(gr.dtype) for gr in grads])
 
 
@@ -174,13 +178,14 @@ class ComputeLoss(nn.Module):
         self.lambda_box, self.lambda_cls, self.lambda_dfl = 7.5, 0.5, 1.5
 
     def forward(self, preds_from_head, targets_collated):
-        out = self.loss_tensor(preds_from_head, targets_collated)
-        vals = out.detach().cpu().tolist()
+        total, terms = self.loss_tensor(preds_from_head, targets_collated)
+        vals = torch.cat([total.detach().view(1), terms]).cpu().tolist()
         items = {"loss_box": vals[1], "loss_cls": vals[2], "loss_dfl": vals[3], "total_loss": vals[0]}
-        return out[0], items
+        return total, items
 
     def loss_tensor(self, preds_from_head, targets_collated):
-        """-> [4] device tensor (total, box, cls, dfl), differentiable in its first entry; no sync."""
+        """-> (total [] device tensor, differentiable; terms [3] device tensor (box, cls, dfl), not
+        differentiable); no host sync."""
         cfg = (self.num_classes, (self.img_size_h, self.img_size_w), self._strides, self.iou_type,
                self.bce_pos_weight, (self.lambda_box, self.lambda_cls, self.lambda_dfl))
         return _DetLossFn.apply(cfg, targets_collated, *preds_from_head)
