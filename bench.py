@@ -148,6 +148,65 @@ def conv_roofline(prof, label):
                 "peak_hbm_gb_s": HBM_PEAK_GBS}}
 
 
+VALU_F32_PEAK_TFLOPS = 157.3    # fp32 vector FMA rate, MI355X_MICROARCH.md chip table
+DW_NAMES = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
+BN_NAMES = ("yms_bn_act_bwd_reduce", "yms_bn_act_bwd_apply", "yms_affine_act", "yms_add_views", "yms_add_grad2")
+
+
+def family_roofline(prof, names, label):
+    """Roofline of a non-MFMA kernel family from one profiled step: algorithmic bytes (each operand
+    once) and FLOPs per launch against the summed HIP-event durations on the launch streams;
+    per launch the attainable time is max(bytes / 8 TB/s, FLOPs / VALU peak)."""
+    rows = {k: v for k, v in prof.items() if k in names}
+    calls = sum(v[0] for v in rows.values())
+    ms = sum(v[1] for v in rows.values())
+    if not calls or ms <= 0:
+        return None
+    fl = sum(v[2] for v in rows.values())
+    nb = sum(v[3] for v in rows.values())
+    t_roof = sum(v[4] for v in rows.values())
+    gbs = nb / (ms * 1e-3) / 1e9
+    return {"bound": "hbm", "achieved": round(gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(gbs / HBM_PEAK_GBS, 4), "kernel": label, "launches": calls,
+            "ms_per_step": round(ms, 4), "algorithmic_mb_per_launch": round(nb / calls / 1e6, 2),
+            "valu_tflops": round(fl / (ms * 1e-3) / 1e12, 2) if fl else None,
+            "per_launch_roofline_frac": round(t_roof / ms, 4),
+            "by_entry_point": {k.replace("yms_", ""): {
+                "launches": v[0], "ms": round(v[1], 4),
+                "gb_s": round(v[3] / (v[1] * 1e-3) / 1e9, 1) if v[1] else 0.0,
+                "roofline_frac": round(v[4] / v[1], 4) if v[1] else 0.0} for k, v in rows.items()}}
+
+
+def step_rooflines(prof, dtype_name, what):
+    """conv (MFMA) roofline + the depthwise and BN/elementwise families' HBM rooflines of one
+    profiled step."""
+    roof = conv_roofline(prof, f"conv implicit-GEMM {what} ({dtype_name} MFMA), one step")
+    dw = family_roofline(prof, DW_NAMES, "depthwise k x k (VALU, fp32 accumulate)")
+    if dw is not None:
+        roof["depthwise"] = dw
+    bn = family_roofline(prof, BN_NAMES, "BN+SiLU affine / BN backward reduce+apply / branch sums")
+    if bn is not None:
+        roof["bn_elementwise"] = bn
+    return roof
+
+
+def train_workload(version, a, world):
+    tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L",
+            "ms-l": "configs[3]: YOLO-MS-L (MS-Block / HKS 3-5-7-9 depthwise graph)",
+            "ms-s": "YOLO-MS-S (MS-Block / HKS graph)"}.get(version, f"custom: YOLO-MS-{version.upper()}")
+    graph = "" if version.startswith("ms-") else f" (reference YOLOv8-'{version}' graph)"
+    allreduce = "bucketed RCCL allreduce+" if world > 1 else ""
+    return (f"{tcfg}{graph} {a.size}x{a.size} {a.dtype} training, B={a.batch}/GPU, fwd+loss+bwd+"
+            f"{allreduce}SGD-nesterov step")
+
+
+def infer_workload(version, a):
+    icfg = {(640, "bf16"): "configs[1]", (1280, "f16"): "configs[4]"}.get((a.size, a.dtype), "custom")
+    if version != "s":
+        icfg += f" (YOLO-MS-{version.upper()} graph)"
+    return f"{icfg}: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU (forward + decode + class-wise NMS)"
+
+
 class MeanSquare(torch.autograd.Function):
     """mean(o^2) of a head map: forward is one fp32-accumulating norm reduction (no fp32 copy of
     o), backward writes d/do = 2*o/numel in one elementwise pass (autograd's vector_norm backward
@@ -237,7 +296,7 @@ def cpu_baseline_train(version, nc, size, batch=8, steps=8, loss="compute", gts=
         step()
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads,
-            "kind": "port", "sample": f"oracle/model_ref.py train step (fwd+{'loss_ref ComputeLoss' if loss == 'compute' else 'surrogate loss'}+bwd+SGD), fp32, B={batch}, "
+            "kind": "port", "sample": f"oracle/{'ms_ref' if version.startswith('ms-') else 'model_ref'}.py train step (fwd+{'loss_ref ComputeLoss' if loss == 'compute' else 'surrogate loss'}+bwd+SGD), fp32, B={batch}, "
             f"{size}x{size}, {steps} timed steps after 1 warmup ({dt:.1f} s), torch threads={threads} "
             f"(OMP_NUM_THREADS share of a host reporting {os.cpu_count()} cpus)"}
 
@@ -261,7 +320,7 @@ def cpu_baseline_infer(version, nc, size, batch=8, steps=12):
         step()
     dt = time.perf_counter() - t0
     return {"value": round(batch * steps / dt, 3), "unit": "images/sec", "cores": threads,
-            "kind": "port", "sample": f"oracle eval forward + C NMS (1 core), fp32, B={batch}, {steps} timed steps "
+            "kind": "port", "sample": f"oracle/{'ms_ref' if version.startswith('ms-') else 'model_ref'}.py eval forward + C NMS (1 core), fp32, B={batch}, {steps} timed steps "
             f"({dt:.1f} s), torch threads={threads}"}
 
 
@@ -308,9 +367,14 @@ def measure_ms_family(a, dev, dtype):
         dt, med = timed(step, steps, warmup, 1)
         out["train"] = {"value": round(a.batch * steps / dt, 2), "unit": "images/sec",
                         "ms_per_step": round(dt / steps * 1e3, 3), "ms_per_step_median": round(med, 3),
-                        "workload": f"{a.ms_version} {a.size}x{a.size} {a.dtype} training, B={a.batch}, "
-                                    "fwd+ComputeLoss+bwd+SGD-nesterov step"}
+                        "workload": train_workload(a.ms_version, a, 1)}
         log(f"[rank 0] {a.ms_version} train: {out['train']['value']} img/s")
+        if not a.no_profile:
+            from yms import _lib
+            _lib.profile_begin()
+            step()
+            out["train"]["roofline"] = step_rooflines(_lib.profile_end(), a.dtype, "fwd+dgrad+wgrad")
+            add_traffic(out["train"]["roofline"], "train", out["train"]["workload"])
         del opt, x
     if a.mode in ("both", "infer") and not a.no_infer:
         torch.manual_seed(0)
@@ -335,10 +399,26 @@ def measure_ms_family(a, dev, dtype):
         dti, medi = timed(istep, steps, warmup, 1)
         out["infer"] = {"value": round(a.infer_batch * steps / dti, 2), "unit": "images/sec",
                         "ms_per_batch": round(dti / steps * 1e3, 3), "ms_per_batch_median": round(medi, 3),
-                        "workload": f"{a.ms_version} {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} "
-                                    "(forward + decode + class-wise NMS)"}
+                        "workload": infer_workload(a.ms_version, a), "nms_overlap": bool(a.nms_overlap)}
         log(f"[rank 0] {a.ms_version} infer: {out['infer']['value']} img/s")
+        if not a.no_profile:
+            from yms import _lib
+            if ns is not None:
+                torch.cuda.current_stream(dev).wait_stream(ns)
+            _lib.profile_begin()
+            istep()
+            out["infer"]["roofline"] = step_rooflines(_lib.profile_end(), a.dtype, "fwd")
+            add_traffic(out["infer"]["roofline"], "infer", out["infer"]["workload"])
     torch.cuda.empty_cache()
+    if not a.no_cpu_baseline:
+        # the MS restatement on host cores (oracle/ms_ref.py: the same torch-CPU ops the reference
+        # graph uses, with depthwise grouped convs): smaller sample, the graph is ~2x YOLOv8-s on CPU
+        log(f"[rank 0] {a.ms_version} cpu baseline...")
+        if "train" in out:
+            out["train"]["cpu_baseline"] = cpu_baseline_train(a.ms_version, a.nc, a.size, batch=8, steps=3,
+                                                              gts=a.gts)
+        if "infer" in out:
+            out["infer"]["cpu_baseline"] = cpu_baseline_infer(a.ms_version, a.nc, a.size, batch=8, steps=4)
     return out
 
 
@@ -479,13 +559,7 @@ def main():
             line["value"] = round(tr["img_s"], 2)
             line["ms_per_step"] = round(tr["dt"] / a.steps * 1e3, 3)
             line["ms_per_step_median"] = round(tr["med_ms"], 3)
-            tcfg = {"s": "configs[2]: YOLO-MS-S", "l": "configs[3]: YOLO-MS-L",
-                    "ms-l": "configs[3]: YOLO-MS-L (MS-Block / HKS 3-5-7-9 depthwise graph)",
-                    "ms-s": "YOLO-MS-S (MS-Block / HKS graph)"}.get(a.version, f"custom: YOLO-MS-{a.version.upper()}")
-            graph = "" if a.version.startswith("ms-") else f" (reference YOLOv8-'{a.version}' graph)"
-            line["config"] = {"workload": f"{tcfg}{graph} "
-                                          f"{a.size}x{a.size} {a.dtype} training, B={a.batch}/GPU, fwd+loss+bwd+"
-                                          "allreduce+SGD-nesterov step",
+            line["config"] = {"workload": train_workload(a.version, a, world),
                               "global_batch": a.batch * world, "per_gpu_batch": a.batch, "img": a.size,
                               "parallelism": f"dp{world}",
                               "loss": (f"ComputeLoss semantics (tools/loss.py:94-677) on the GPU, {a.gts} synthetic "
@@ -496,21 +570,16 @@ def main():
                               "peak_hbm_gib": round(tr["peak_gb"], 2),
                               "hip_graph": tr["graph"]}
             if "train_prof" in result:
-                line["roofline"] = conv_roofline(result["train_prof"], "conv implicit-GEMM fwd+dgrad+wgrad "
-                                                 f"({a.dtype} MFMA), one training step")
+                line["roofline"] = step_rooflines(result["train_prof"], a.dtype, "fwd+dgrad+wgrad")
                 add_traffic(line["roofline"], "train", line["config"]["workload"])
         if "infer" in result:
-            icfg = {(640, "bf16"): "configs[1]", (1280, "f16"): "configs[4]"}.get((a.size, a.dtype), "custom")
-            if a.version != "s":
-                icfg += f" (YOLO-MS-{a.version.upper()} graph)"
             inf = {"value": round(result["infer"]["img_s"], 2), "unit": "images/sec",
                    "ms_per_batch": round(result["infer"]["dt"] / a.steps * 1e3, 3),
                    "ms_per_batch_median": round(result["infer"]["med_ms"], 3),
-                   "workload": f"{icfg}: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU "
-                               "(forward + decode + class-wise NMS)", "hip_graph": result["infer"]["graph"],
+                   "workload": infer_workload(a.version, a), "hip_graph": result["infer"]["graph"],
                    "nms_overlap": bool(a.nms_overlap)}
             if "infer_prof" in result:
-                inf["roofline"] = conv_roofline(result["infer_prof"], f"conv implicit-GEMM fwd ({a.dtype} MFMA)")
+                inf["roofline"] = step_rooflines(result["infer_prof"], a.dtype, "fwd")
                 add_traffic(inf["roofline"], "infer", inf["workload"])
             line["infer"] = inf
             if "value" not in line:

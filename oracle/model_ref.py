@@ -162,6 +162,29 @@ def init_params(version, nc):
     return sd
 
 
+def ordered_init(sd, seed=0, gamma=0.3):
+    """Well-conditioned variant of a closed-form state dict (tests only): conv weights He-normal
+    from a seeded generator, BN gammas around ``gamma`` (closed form, +-25%).
+
+    The closed-form sin() weights are strongly correlated along the flattened index, and with BN
+    gammas ~1 the deep graphs sit in a chaotic regime where forward rounding differences grow
+    ~2x per 10 BN layers: torch's own CPU fp32 gradients then miss fp64 by up to 1e-1 (ms-l at
+    640: median 0.56), so a gradient gate measures the graph, not the kernels.  With these
+    weights the CPU fp32 gradients sit within ~6e-5 of fp64 on every graph the tests train (n, s,
+    l, ms-xs, ms-s, ms-l; tools/cond_sweep.py), and absolute / 1.3x-of-CPU-bf16 gates apply."""
+    g = torch.Generator().manual_seed(seed)
+    out = OrderedDict()
+    for k, t in sd.items():
+        if k.endswith("conv.weight") and k != "head.dfl.conv.weight" or (k.startswith("head.") and k.endswith(".2.weight")):
+            fan = t.shape[1] * t.shape[2] * t.shape[3]
+            out[k] = torch.randn(tuple(t.shape), generator=g) * math.sqrt(2.0 / fan)
+        elif k.endswith("bn.weight"):
+            out[k] = _closed_form(k, tuple(t.shape), 0.25 * gamma, base=gamma)
+        else:
+            out[k] = t.clone()
+    return out
+
+
 # ----------------------------------------------------------------------------
 # Functional graph
 # ----------------------------------------------------------------------------

@@ -46,38 +46,6 @@ def _quantiles(errs, qs=(0.5, 0.9, 1.0)):
     return [torch.quantile(t, q).item() for q in qs]
 
 
-@pytest.mark.parametrize("v,h,w", [("ms-xs", 320, 320), ("ms-s", 256, 256)])
-def test_ms_fp32_train_grads_drift_vs_cpu_fp32(v, h, w):
-    """Training step of the whole YOLO-MS graph in fp32.  At random init the deep MS stacks
-    (BN over few pixels at stride 32, hierarchical residual sums) are so ill-conditioned that
-    torch's own CPU fp32 gradients sit 0.03-7% from fp64 (tools/ms_diag.py; ms-xs below 128^2 swings
-    by 30x between input seeds), so the gate is
-    relative: per-parameter gradient error vs fp64 at the median / p90 / max within 4x of the
-    CPU fp32 oracle's, head maps and BN running buffers within 4x too.  The per-component
-    tightness is pinned by the standalone MS-Block test below (1e-4)."""
-    nc = 80
-    sd = MS.init_params(v, nc)
-    x = torch.randn(2, 3, h, w, generator=torch.Generator().manual_seed(41))
-    p32, r32 = _grads(v, nc, sd, x, torch.float32)
-    p64, r64 = _grads(v, nc, sd, x, torch.float64)
-    m = _model(v, nc, sd).train()
-    outs = m(x.to(DEV))
-    for o, a, b in zip(outs, r32, r64):
-        assert _rel(o.detach(), b.detach()) <= 4 * _rel(a.detach(), b.detach()) + 1e-6
-    sum((o.double() ** 2).mean() for o in outs).backward()
-    pd = dict(m.named_parameters())
-    keys = [k for k, t in p64.items() if t.grad is not None]
-    assert len(keys) == len([q for q in pd.values() if q.requires_grad])
-    ours = _quantiles([_rel(pd[k].grad, p64[k].grad) for k in keys])
-    cpu = _quantiles([_rel(p32[k].grad, p64[k].grad) for k in keys])
-    for q, a, b in zip((0.5, 0.9, 1.0), ours, cpu):
-        assert a <= 4 * b + 1e-5, (q, a, b)
-    bufs = dict(m.named_buffers())
-    for k, t in p64.items():
-        if "running" in k:
-            assert _rel(bufs[k], t) <= 4 * _rel(p32[k], t) + 1e-4, k
-
-
 def test_msblock_module_hks9_fp32_and_bf16():
     """One MS-Block with the largest HKS kernel (k = 9, two IB layers per branch) as a standalone
     module (well conditioned: 1920 pixels per BN): forward, input and parameter gradients in fp32

@@ -168,3 +168,58 @@ def test_stem_wgrad_with_fused_bn_backward(dt, n, h, w, cout):
     out = dw.double().cpu()
     rel = ((out - ref).norm() / ref.norm()).item()
     assert rel < 2e-3, rel
+
+
+def test_stem_b64_640_fwd_stats_and_wgrad():
+    """The bench's stem: 64 x 3 x 640 x 640 fp32 input -> 32 channels at 320^2 (configs[2]), in bf16.
+    Forward z and its BN statistics (25,600 partial rows) vs an fp32 im2col GEMM on the GPU, and the
+    weight gradient with the fused BN+SiLU backward apply vs an fp32 GEMM over the same dz."""
+    import torch.nn.functional as F
+    from hiputil import check_moments, split_stats, stats_buffer
+    n, h, w, cout, dt = 64, 640, 640, 32, torch.bfloat16
+    dev = "cuda"
+    g = torch.Generator(device=dev).manual_seed(64)
+    x = torch.randn(n, 3, h, w, device=dev, generator=g)
+    wt = torch.randn(cout, 3, 3, 3, device=dev, generator=g) * 0.3
+    sh_ = shape(n, h, w, 3, cout, 3, 2, dt)
+    sp = ctypes.pointer(sh_)
+    ho, wo = sh_.ho, sh_.wo
+    rows, ld_s = L.lib().yms_conv_stem_stats_rows(sp), L.lib().yms_conv_stats_ld(sp)
+    buf = stats_buffer(rows, ld_s)
+    z = torch.empty((n, ho, wo, r8(cout)), dtype=dt, device=dev)
+    L.call("yms_conv_stem_fwd", sp, x.data_ptr(), wt.data_ptr(), z.data_ptr(), r8(cout), 0, None, None,
+           L.ACT_NONE, buf.data_ptr(), ld_s, L.stream_ptr())
+    xr, wr = x.to(dt).float(), wt.to(dt).float()
+    cols = F.unfold(xr, 3, padding=1, stride=2)                              # [n, 27, ho*wo]
+    ref = (wr.view(cout, -1) @ cols).view(n, cout, ho, wo)
+    zz = z[..., :cout].permute(0, 3, 1, 2).float()
+    assert (zz - ref).abs().max().item() <= 8e-3 * ref.abs().max().item()
+    check_moments(split_stats(buf, rows, ld_s), ref, 1e-4)
+    del buf
+    # backward: dz = BN+SiLU backward apply (fp32, rounded to bf16) of (gy, z), then dW = dz^T im2col(x)
+    gy = (torch.randn(n, ho, wo, cout, device=dev, generator=g) * 0.1).to(dt)
+    sc = torch.rand(cout, device=dev, generator=g) + 0.5
+    sf = torch.randn(cout, device=dev, generator=g) * 0.2
+    mu = torch.randn(cout, device=dev, generator=g) * 0.1
+    istd = torch.rand(cout, device=dev, generator=g) + 0.5
+    coef = torch.randn(2 * cout, device=dev, generator=g) * 0.05
+    zf, gf = z[..., :cout].float(), gy.float()
+    a = zf * sc + sf
+    s_ = torch.sigmoid(a)
+    da = gf * (s_ * (1 + a * (1 - s_)))
+    bz = -sc * coef[cout:] * istd
+    a0 = -sc * coef[:cout] - bz * mu
+    dz = (sc * da + a0 + bz * zf).to(dt).float()                            # [n, ho, wo, cout]
+    del a, s_, da
+    ref_dw = torch.einsum("nlo,nkl->ok", dz.reshape(n, ho * wo, cout), cols).view(cout, 3, 3, 3)
+    del cols, dz
+    ws = torch.empty(L.lib().yms_conv_stem_wgrad_ws_bytes(sp) // 4 + 1, device=dev)
+    dw = torch.full((cout, 3, 3, 3), float("nan"), device=dev)
+    mi = torch.cat([mu, istd])
+    zc = z.contiguous()
+    L.call("yms_conv_stem_wgrad", sp, x.data_ptr(), gy.data_ptr(), cout, 0, zc.data_ptr(), r8(cout), 0, sc.data_ptr(),
+           sf.data_ptr(), mi.data_ptr(), coef.data_ptr(), L.ACT_SILU, ws.data_ptr(), ws.numel() * 4, dw.data_ptr(), 0,
+           L.stream_ptr())
+    torch.cuda.synchronize()
+    rel = ((dw.double() - ref_dw.double()).norm() / ref_dw.double().norm()).item()
+    assert rel < 2e-3, rel

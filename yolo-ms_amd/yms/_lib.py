@@ -141,9 +141,45 @@ def check(status, what):
 
 _prof = None
 _CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd")
+_DW = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
+# launches whose hipStream_t is the last argument (status-returning entry points ending in a void*)
+_STREAM_LAST = {n for n, (res, args) in _SIGS.items() if res is _I and args and args[-1] is _P}
 
 
 _FN = {}
+
+
+def _elt(dt):
+    return 4 if dt == F32 else 2
+
+
+def _work(name, args):
+    """(algorithmic FLOPs, algorithmic HBM bytes) of one launch: every operand read or written once.
+    Convs: input + output + weights (fp32 weight gradient); depthwise: the same with fp32 [C][k][k]
+    weights (FLOPs = 2 n h w c k^2, VALU); BN / branch-sum elementwise passes: their streams."""
+    if name in _CONV:
+        sh = args[0].contents
+        fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
+        es = _elt(sh.dtype)
+        act = (sh.n * sh.h * sh.w * sh.cin + sh.n * sh.ho * sh.wo * sh.cout) * es
+        return fl, act + sh.cout * sh.cin * sh.k * sh.k * (4 if name == "yms_conv_wgrad" else es)
+    if name in _DW:
+        d = args[0].contents
+        vol = d.n * d.h * d.w * d.c
+        return 2 * vol * d.k * d.k, 2 * vol * _elt(d.dtype) + 4 * d.c * d.k * d.k
+    if name in ("yms_bn_act_bwd_reduce", "yms_affine_act", "yms_bn_act_bwd_apply", "yms_add_views",
+                "yms_add_grad2"):
+        vol = args[1] * args[2] * _elt(args[0])
+        if name == "yms_bn_act_bwd_reduce":
+            return 0, 2 * vol                                          # z, gy
+        if name == "yms_affine_act":
+            return 0, (2 + (args[9] is not None)) * vol                # z (+res) -> y
+        if name == "yms_bn_act_bwd_apply":
+            return 0, (3 + (args[17] is not None) * (1 + bool(args[20]))) * vol   # z, gy -> dz (+ gres)
+        if name == "yms_add_views":
+            return 0, (2 + (args[6] is not None) + bool(args[12])) * vol
+        return 0, (3 + bool(args[9]) + bool(args[13])) * vol       # add_grad2: gy -> ga, gb
+    return 0, 0
 
 
 def call(name, *args):
@@ -157,20 +193,13 @@ def call(name, *args):
         return
     s = torch.cuda.Event(enable_timing=True)
     e = torch.cuda.Event(enable_timing=True)
-    # conv entry points take their hipStream_t last: time them on the stream they run on
-    # (wgrad runs on the backward's side stream)
-    st = torch.cuda.ExternalStream(args[-1]) if name in _CONV and args[-1] else None
+    # entry points take their hipStream_t last: time them on the stream they run on (weight
+    # gradients run on the backward's side stream)
+    st = torch.cuda.ExternalStream(args[-1]) if name in _STREAM_LAST and args[-1] else None
     s.record(st)
     check(getattr(lib(), name)(*args), name)
     e.record(st)
-    fl = nb = 0
-    if name in _CONV:
-        sh = args[0].contents
-        fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
-        # algorithmic HBM bytes: each operand once (input, output, weights; fp32 weight gradient)
-        es = 4 if sh.dtype == F32 else 2
-        act = (sh.n * sh.h * sh.w * sh.cin + sh.n * sh.ho * sh.wo * sh.cout) * es
-        nb = act + sh.cout * sh.cin * sh.k * sh.k * (4 if name == "yms_conv_wgrad" else es)
+    fl, nb = _work(name, args)
     _prof.append((name, s, e, fl, nb))
 
 
@@ -181,10 +210,11 @@ def profile_begin():
     _prof = []
 
 
-def profile_end(peak_tflops=2500.0, peak_gbs=8000.0):
+def profile_end(peak_tflops=2500.0, peak_gbs=8000.0, valu_tflops=157.3):
     """-> {name: [calls, total_ms, flops, bytes, roofline_ms, hbm_bound_calls]} for the launches
-    since profile_begin().  roofline_ms sums, per launch, max(flops / peak_tflops, bytes /
-    peak_gbs): the time the launch would take at the roofline of its own arithmetic intensity."""
+    since profile_begin().  roofline_ms sums, per launch, max(flops / peak, bytes / peak_gbs): the
+    time the launch would take at the roofline of its own arithmetic intensity (peak = the dense
+    MFMA rate for convs, the fp32 VALU rate for the depthwise kernels)."""
     global _prof
     torch.cuda.synchronize()
     out = {}
@@ -194,7 +224,8 @@ def profile_end(peak_tflops=2500.0, peak_gbs=8000.0):
         r[1] += s.elapsed_time(e)
         r[2] += fl
         r[3] += nb
-        t_f, t_b = fl / (peak_tflops * 1e9), nb / (peak_gbs * 1e6)   # ms
+        pk = valu_tflops if name in _DW else peak_tflops
+        t_f, t_b = fl / (pk * 1e9), nb / (peak_gbs * 1e6)   # ms
         r[4] += max(t_f, t_b)
         r[5] += int(t_b > t_f)
     _prof = None

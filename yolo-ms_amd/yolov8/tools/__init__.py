@@ -1,5 +1,7 @@
-"""The reference's tools/ (dataset, training loop, loss, utils) are outside the hot path;
-with ``YMS_REFERENCE_ROOT`` set they resolve from the reference checkout."""
+"""``yolov8.tools``: ``loss`` here is the fused GPU ComputeLoss (tools/loss.py:94-677 interface) and
+always shadows the reference's module of the same name.  The reference's other tools (dataset,
+training loop, utils: outside the hot path) resolve from the reference checkout when
+``YMS_REFERENCE_ROOT`` is set; the input pipeline's GPU half is ``yms.data``."""
 import os as _os
 
 _ref = _os.environ.get("YMS_REFERENCE_ROOT")
