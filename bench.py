@@ -202,7 +202,9 @@ def train_workload(version, a, world):
 
 def infer_workload(version, a):
     icfg = {(640, "bf16"): "configs[1]", (1280, "f16"): "configs[4]"}.get((a.size, a.dtype), "custom")
-    if version != "s":
+    if version.startswith("ms-"):
+        icfg += f" (YOLO-MS-{version[3:].upper()} MS-Block / HKS graph)"
+    elif version != "s":
         icfg += f" (YOLO-MS-{version.upper()} graph)"
     return f"{icfg}: {a.size}x{a.size} {a.dtype} inference B={a.infer_batch} on 1 GPU (forward + decode + class-wise NMS)"
 

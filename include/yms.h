@@ -256,6 +256,17 @@ yms_status yms_map_accumulate(int n_det, const float* scores, const int* labels,
  * rounding is not reproduced). */
 yms_status yms_resize_normalize(int dtype, int n, const void* images, int out_h, int out_w, const float* mean,
                                 const float* std, void* out, void* stream);
+/* The training transform (dataset.py:84-131: HueSaturationValue, Rotate, ShiftScaleRotate, RandomScale,
+ * Affine shear, Perspective, flips, then Resize + Normalize + ToTensorV2 + stack), batched: images =
+ * device array of n AugImage records (yms_augment_image_bytes() bytes each; layout in
+ * csrc/preprocess.hip / yms.data.AugImage): the decoded HWC uint8 source, an optional HSV shift
+ * (cv2 8-bit HSV, albumentations LUT semantics) and up to 8 geometric stages, each a 3x3 matrix
+ * from its output pixel-index coordinates to its input frame plus that frame's size and border rule
+ * (reflect-101 / clamp / constant 0).  The per-image parameters are sampled on the host
+ * (yms.data.sample_augmentation); one bilinear sample of the source per output pixel. */
+size_t yms_augment_image_bytes(void);
+yms_status yms_augment_normalize(int dtype, int n, const void* images, int out_h, int out_w, const float* mean,
+                                 const float* std, void* out, void* stream);
 
 /* ---- detection loss ------------------------------------------------------- */
 /* The reference's ComputeLoss (yolov8/tools/loss.py:94-677; python binding

@@ -89,9 +89,10 @@ def check_moments(st, z, tol):
     c = z.shape[1]
     npix = z.numel() // c
     s1, m2 = merge_moments(st, c, npix)
-    zd = z.double()
-    ref1 = zd.sum((0, 2, 3))
-    ref2 = ((zd - zd.mean((0, 2, 3), keepdim=True)) ** 2).sum((0, 2, 3))
+    zd = z.double()                       # on z's device; only the per-channel sums come back
+    ref1 = zd.sum((0, 2, 3)).cpu()
+    ref2 = ((zd - zd.mean((0, 2, 3), keepdim=True)) ** 2).sum((0, 2, 3)).cpu()
+    del zd
     e1 = ((s1 - ref1).abs().max() / (ref1.abs().max() + 1e-6)).item()
     e2 = ((m2 - ref2).abs() / ref2.clamp_min(1e-30)).max().item()
     assert e1 <= tol and e2 <= tol, (e1, e2)

@@ -238,3 +238,44 @@ def _halo_case(shp):
                    dx.shape[-1], 0, acc, L.stream_ptr())
             exp = xr.grad + (base.to(dtype).float() if acc else 0)
             _close(nchw(dx, cin).cpu(), exp, TOL["bf16"] * 2)
+
+
+# halo-tiled 3x3 weight gradient (wgrad_halo.hip): patch widths TW = W (W <= 40), divisors of W,
+# W not a multiple of TW; stride 1 / 2 with odd sizes (halo clipping at every border); cout of one
+# or two 32-blocks with padding (16, 48, 80, 130); cin not a multiple of 32 (8, 40, 96); many
+# patches per split (n = 6); images spanning patch rows.
+WGH = [
+    (2, 32, 20, 20, 32, 1), (3, 40, 13, 27, 48, 1), (2, 64, 80, 80, 64, 1), (1, 96, 50, 70, 80, 1),
+    (2, 8, 33, 41, 16, 2), (2, 64, 40, 40, 130, 2), (1, 32, 161, 97, 64, 2), (6, 64, 24, 24, 64, 1),
+    (1, 16, 7, 300, 32, 1), (2, 48, 9, 5, 40, 2),
+]
+
+
+@pytest.mark.parametrize("mode", ["2", "1"])
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("shp", WGH)
+def test_wgrad_3x3_halo(shp, dt, mode, monkeypatch):
+    """mode 2 forces the halo kernel on every shape; mode 1 is the default selection (halo for
+    stride-1 layers with 32 / 64 output channels, the im2col kernel otherwise)."""
+    monkeypatch.setenv("YMS_WG_HALO", mode)
+    n, cin, h, w, cout, s = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(n * 7919 + cin * 31 + h + w + cout + s)
+    x = torch.randn(n, cin, h, w, generator=g)
+    shp_ = shape(n, h, w, cin, cout, 3, s, dtype)
+    dz = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+    xr, dzr = x.to(dtype).double(), dz.to(dtype).double()
+    ref = torch.nn.grad.conv2d_weight(xr, (cout, cin, 3, 3), dzr, stride=s, padding=1)
+    sp = ctypes.pointer(shp_)
+    # channel slots of wider buffers (x at offset 8, dz at offset 16)
+    xb = nhwc(x, dtype, ld=r8(cin) + 16, off=8)
+    dzb = nhwc(dz, dtype, ld=r8(cout) + 16, off=16)
+    wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
+    ws = torch.full((wsb // 4 + 1,), float("nan"), dtype=torch.float32, device="cuda")
+    for acc in (0, 1):
+        dw = torch.full((cout, cin, 3, 3), 0.25, device="cuda")
+        L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 8, dzb.data_ptr(), dzb.shape[-1], 16,
+               ws.data_ptr(), wsb, dw.data_ptr(), acc, L.stream_ptr())
+        got = dw.double().cpu() - (0.25 if acc else 0.0)
+        rel = ((got - ref).norm() / ref.norm()).item()
+        assert rel < 1e-5 and (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, (acc, rel)

@@ -26,6 +26,13 @@ if os.environ.get("YMS_MICRO_SHAPES") == "ms":   # YOLO-MS-S MS-Block 1x1 convs 
               (64, 160, 160, 96, 64, 1, 1), (64, 80, 80, 128, 192, 1, 1), (64, 80, 80, 64, 128, 1, 1),
               (64, 80, 80, 128, 64, 1, 1), (64, 80, 80, 192, 128, 1, 1), (64, 40, 40, 128, 256, 1, 1),
               (64, 40, 40, 256, 128, 1, 1)]
+if os.environ.get("YMS_MICRO_SHAPES") == "wg":   # every distinct 3x3 layer of YOLOv8-s at 640 (B=64)
+    SHAPES = [(64, 640, 640, 3, 32, 3, 2), (64, 320, 320, 32, 64, 3, 2), (64, 160, 160, 32, 32, 3, 1),
+              (64, 160, 160, 64, 128, 3, 2), (64, 80, 80, 64, 64, 3, 1), (64, 80, 80, 128, 256, 3, 2),
+              (64, 40, 40, 128, 128, 3, 1), (64, 40, 40, 256, 512, 3, 2), (64, 20, 20, 256, 256, 3, 1),
+              (64, 80, 80, 128, 128, 3, 2), (64, 40, 40, 256, 256, 3, 2), (64, 80, 80, 128, 64, 3, 1),
+              (64, 80, 80, 128, 80, 3, 1), (64, 80, 80, 80, 80, 3, 1), (64, 40, 40, 256, 64, 3, 1),
+              (64, 40, 40, 256, 80, 3, 1), (64, 20, 20, 512, 64, 3, 1), (64, 20, 20, 512, 80, 3, 1)]
 dt = torch.bfloat16
 st = L.stream_ptr()
 

@@ -18,6 +18,7 @@
 // partial slabs that a second kernel reduces deterministically (no atomics).
 #include "conv_common.hpp"
 #include "conv_halo.hpp"
+#include "wgrad_halo.hpp"
 
 namespace yms {
 
@@ -1636,6 +1637,8 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
 
 size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
+  WHPlan wh;
+  if (wgrad_halo_plan(s, &wh)) return (size_t)wh.splits * wh.wk * wh.slab_rows * wh.slab_ld * sizeof(float);
   WgradPlan w = wgrad_plan(s);
   return (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float);
 }
@@ -1645,6 +1648,21 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
                           float* dw, int accumulate, void* stream) {
   if (!shape_ok(s) || !x || !dz || !ws || !dw) return YMS_ERR_INVALID;
   if (!view_ok(x_ld, x_off, s->cin) || !view_ok(dz_ld, dz_off, s->cout)) return YMS_ERR_INVALID;
+  {
+    // 3x3: the halo-tiled kernel (wgrad_halo.hip) stages each input patch once for all nine taps
+    WHPlan wh;
+    if (wgrad_halo_plan(s, &wh)) {
+      if (ws_bytes < (size_t)wh.splits * wh.wk * wh.slab_rows * wh.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
+      yms_status e = wgrad_halo_launch(s, wh, x, x_ld, x_off, dz, dz_ld, dz_off, ws, (hipStream_t)stream);
+      if (e != YMS_OK) return e;
+      const int cin8 = (int)rup(s->cin, 8);
+      const int kf = 9 * cin8;
+      dim3 g2((unsigned)(s->cout * cdiv(kf, 128)));
+      hipLaunchKernelGGL(wgrad_reduce_kernel, g2, dim3(256), 0, (hipStream_t)stream, ws, wh.splits * wh.wk,
+                         (long)wh.slab_rows * wh.slab_ld, wh.slab_ld, s->cout, s->cin, cin8, s->k, dw, accumulate);
+      return launch_status();
+    }
+  }
   WgradPlan w = wgrad_plan(s);
   if (ws_bytes < (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
   TTParams p{};

@@ -103,6 +103,8 @@ _SIGS = {
     "yms_det_loss_ws_bytes": (_SZ, [_I, _I, _I, _I]),
     "yms_stream_create_cu_subset": (_I, [_I, _I, ctypes.POINTER(ctypes.c_void_p)]),
     "yms_resize_normalize": (_I, [_I, _I, _P, _I, _I, _P, _P, _P, _P]),
+    "yms_augment_image_bytes": (_SZ, []),
+    "yms_augment_normalize": (_I, [_I, _I, _P, _I, _I, _P, _P, _P, _P]),
     "yms_det_loss": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I, _F, _F, _I, _P, _P, _P, _SZ, _P, _P]),
     "yms_head_decode": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P]),
     "yms_dfl": (_I, [_I, _I, _I, _I, _P, _P, _P]),

@@ -11,8 +11,19 @@ collated to ``[M, 6]`` with the batch index first (dataset.py:235-267).
 
 Annotations are read with the ``json`` module in pycocotools' orders (image ids sorted, category
 ids in file order, annotations per image in file order); pycocotools, albumentations and cv2 are
-not installed here.  Training colour / geometric augmentations other than the flips
-(dataset.py:92-127) are not reproduced.
+not installed here.
+
+Training augmentation (dataset.py:84-131, the albumentations chain HueSaturationValue -> Rotate ->
+ShiftScaleRotate -> RandomScale -> Affine(shear) -> Perspective -> HorizontalFlip / VerticalFlip ->
+Resize -> Normalize with BboxParams(coco, min_visibility 0.1, min_area 1)) is restated:
+``sample_augmentation`` draws each image's transforms on the host in that order with
+albumentations' probabilities and parameter distributions, composes them into a chain of
+pixel-coordinate stages, and ``augment_normalize`` applies the whole chain plus Normalize in ONE
+GPU launch (csrc/preprocess.hip: one bilinear sample per output pixel instead of one resampling
+per transform); ``transform_boxes`` moves the COCO boxes through the same stages (corner
+envelopes, clipped once at the end, then the visibility / area filters).  albumentations and cv2
+are not installed, so parity with them is UNPINNED; the GPU kernel is pinned
+to the restatement in oracle/preprocess_ref.py.
 """
 from __future__ import annotations
 
@@ -77,6 +88,210 @@ def resize_normalize(images, size, mean=IMAGENET_MEAN, std=IMAGENET_STD, flips=N
         im.record_stream(torch.cuda.current_stream(dev))
     tab_dev.record_stream(torch.cuda.current_stream(dev))
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# training augmentation (dataset.py:84-131)
+# ------------------------------------------------------------------------------------------
+AUG_REFLECT101, AUG_CLAMP, AUG_CONSTANT = 0, 1, 2
+AUG_MAX_STAGES = 8
+
+
+class AugStage(ctypes.Structure):
+    """One geometric stage: m maps OUTPUT pixel-index coordinates to the input frame (in_w x in_h)."""
+    _fields_ = [("m", ctypes.c_float * 9), ("in_w", ctypes.c_int), ("in_h", ctypes.c_int),
+                ("border", ctypes.c_int), ("pad_", ctypes.c_int)]
+
+
+class AugImage(ctypes.Structure):
+    """csrc/preprocess.hip AugImage (checked against yms_augment_image_bytes())."""
+    _fields_ = [("src", ctypes.c_void_p), ("h", ctypes.c_int), ("w", ctypes.c_int), ("pitch", ctypes.c_int),
+                ("nst", ctypes.c_int), ("hsv", ctypes.c_float * 3), ("do_hsv", ctypes.c_int),
+                ("st", AugStage * AUG_MAX_STAGES)]
+
+
+class AugPlan:
+    """One image's sampled transform: optional HSV shift (LUT units) and geometric stages, each
+    (F, in_w, in_h, out_w, out_h, border) with F the 3x3 FORWARD map of pixel-index coordinates
+    (input -> output; homogeneous)."""
+
+    def __init__(self, h, w):
+        self.src_h, self.src_w = h, w
+        self.hsv = None
+        self.stages = []
+        self.applied = []          # names of the transforms drawn (diagnostics / tests)
+
+    @property
+    def frame(self):
+        if self.stages:
+            return self.stages[-1][3], self.stages[-1][4]
+        return self.src_w, self.src_h
+
+    def add(self, F, out_w, out_h, border, name):
+        in_w, in_h = self.frame
+        self.stages.append((np.asarray(F, np.float64), in_w, in_h, int(out_w), int(out_h), border))
+        self.applied.append(name)
+
+
+def _rot_matrix(cx, cy, deg, scale=1.0):
+    """cv2.getRotationMatrix2D(center, angle, scale) as a 3x3 (positive angle = counter-clockwise)."""
+    a = np.deg2rad(deg)
+    al, be = scale * np.cos(a), scale * np.sin(a)
+    return np.array([[al, be, (1 - al) * cx - be * cy], [-be, al, be * cx + (1 - al) * cy], [0, 0, 1]])
+
+
+def _resize_matrix(in_w, in_h, out_w, out_h):
+    """cv2.resize INTER_LINEAR pixel-centre map, input index -> output index."""
+    sx, sy = in_w / out_w, in_h / out_h
+    return np.array([[1 / sx, 0, 0.5 / sx - 0.5], [0, 1 / sy, 0.5 / sy - 0.5], [0, 0, 1]])
+
+
+def _homography(src, dst):
+    """cv2.getPerspectiveTransform: the 3x3 H with dst ~ H src for four point pairs."""
+    A, b = [], []
+    for (x, y), (u, v) in zip(src, dst):
+        A.append([x, y, 1, 0, 0, 0, -u * x, -u * y])
+        A.append([0, 0, 0, x, y, 1, -v * x, -v * y])
+        b += [u, v]
+    h = np.linalg.solve(np.asarray(A, np.float64), np.asarray(b, np.float64))
+    return np.append(h, 1.0).reshape(3, 3)
+
+
+def sample_augmentation(rng, tp, h, w, out_h, out_w, is_train=True):
+    """dataset.py:89-131 for one image of h x w pixels: each transform of the training list is
+    drawn with albumentations' probability (p = 0.5; the flips p = fliplr / flipud) and parameter
+    distribution, in list order, from the numpy Generator ``rng``; then the final Resize.
+    tp: the config's augmentation dict (hsv_h/s/v, degrees, translate, scale, shear, perspective,
+    fliplr, flipud)."""
+    tp = tp or {}
+    plan = AugPlan(h, w)
+    if is_train:
+        hl, sl, vl = (int(tp.get(k, 0) * 100) for k in ("hsv_h", "hsv_s", "hsv_v"))
+        if tp.get("hsv_h", 0) > 0 or tp.get("hsv_s", 0) > 0 or tp.get("hsv_v", 0) > 0:
+            if rng.random() < 0.5:     # A.HueSaturationValue(hue_shift_limit, sat_shift_limit, val_shift_limit)
+                plan.hsv = (rng.uniform(-hl, hl), rng.uniform(-sl, sl), rng.uniform(-vl, vl))
+                plan.applied.append("hsv")
+        if tp.get("degrees", 0) > 0 and rng.random() < 0.5:       # A.Rotate(limit=degrees), reflect-101
+            fw, fh = plan.frame
+            ang = rng.uniform(-tp["degrees"], tp["degrees"])
+            plan.add(_rot_matrix((fw - 1) / 2, (fh - 1) / 2, ang), fw, fh, AUG_REFLECT101, "rotate")
+        if tp.get("translate", 0) > 0 and rng.random() < 0.5:     # A.ShiftScaleRotate(shift only), reflect-101
+            fw, fh = plan.frame
+            t = tp["translate"]
+            dx, dy = rng.uniform(-t, t), rng.uniform(-t, t)
+            plan.add(np.array([[1, 0, dx * fw], [0, 1, dy * fh], [0, 0, 1]]), fw, fh, AUG_REFLECT101, "shift")
+        if tp.get("scale", 0) > 0 and rng.random() < 0.5:         # A.RandomScale(scale_limit): resized frame
+            fw, fh = plan.frame
+            sc = rng.uniform(1 - tp["scale"], 1 + tp["scale"])
+            nw, nh = max(1, int(fw * sc)), max(1, int(fh * sc))
+            plan.add(_resize_matrix(fw, fh, nw, nh), nw, nh, AUG_CLAMP, "scale")
+        if tp.get("shear", 0) > 0 and rng.random() < 0.5:         # A.Affine(shear x / y in degrees), constant 0
+            fw, fh = plan.frame
+            shx, shy = (np.tan(np.deg2rad(rng.uniform(-tp["shear"], tp["shear"]))) for _ in range(2))
+            cx, cy = (fw - 1) / 2, (fh - 1) / 2
+            Sm = np.array([[1, shx, 0], [shy, 1, 0], [0, 0, 1]])
+            T0 = np.array([[1, 0, -cx], [0, 1, -cy], [0, 0, 1]])
+            T1 = np.array([[1, 0, cx], [0, 1, cy], [0, 0, 1]])
+            plan.add(T1 @ Sm @ T0, fw, fh, AUG_CONSTANT, "shear")
+        if tp.get("perspective", 0) > 0 and rng.random() < 0.5:   # A.Perspective(scale=(0, p)), keep_size
+            fw, fh = plan.frame
+            sc = rng.uniform(0, tp["perspective"])
+            j = np.mod(np.abs(rng.normal(0, sc, (4, 2))), 0.32)
+            quad = [(j[0, 0] * fw, j[0, 1] * fh), ((1 - j[1, 0]) * fw, j[1, 1] * fh),
+                    ((1 - j[2, 0]) * fw, (1 - j[2, 1]) * fh), (j[3, 0] * fw, (1 - j[3, 1]) * fh)]
+            quad = [(x - 0.5, y - 0.5) for x, y in quad]
+            rect = [(0, 0), (fw - 1, 0), (fw - 1, fh - 1), (0, fh - 1)]
+            plan.add(_homography(quad, rect), fw, fh, AUG_CONSTANT, "perspective")
+        if tp.get("fliplr", 0) > 0 and rng.random() < tp["fliplr"]:
+            fw, fh = plan.frame
+            plan.add(np.array([[-1, 0, fw - 1], [0, 1, 0], [0, 0, 1]]), fw, fh, AUG_CLAMP, "fliplr")
+        if tp.get("flipud", 0) > 0 and rng.random() < tp["flipud"]:
+            fw, fh = plan.frame
+            plan.add(np.array([[1, 0, 0], [0, -1, fh - 1], [0, 0, 1]]), fw, fh, AUG_CLAMP, "flipud")
+    fw, fh = plan.frame
+    plan.add(_resize_matrix(fw, fh, out_w, out_h), out_w, out_h, AUG_CLAMP, "resize")
+    if len(plan.stages) > AUG_MAX_STAGES:
+        raise RuntimeError("yms: augmentation chain longer than AUG_MAX_STAGES")
+    return plan
+
+
+def plan_struct(plan, image):
+    """AugImage record of one plan over a device HWC uint8 image tensor."""
+    rec = AugImage()
+    rec.src = image.data_ptr()
+    rec.h, rec.w, rec.pitch = image.shape[0], image.shape[1], image.stride(0)
+    if (rec.h, rec.w) != (plan.src_h, plan.src_w):
+        raise ValueError("yms: augmentation plan sampled for another image size")
+    rec.nst = len(plan.stages)
+    if plan.hsv is not None:
+        rec.do_hsv = 1
+        rec.hsv[:] = [float(v) for v in plan.hsv]
+    for k, (F, in_w, in_h, _, _, border) in enumerate(plan.stages):
+        M = np.linalg.inv(F)
+        M = M / M[2, 2] if abs(M[2, 2]) > 1e-12 else M
+        rec.st[k].m[:] = [float(v) for v in M.reshape(-1)]
+        rec.st[k].in_w, rec.st[k].in_h, rec.st[k].border = in_w, in_h, border
+    return rec
+
+
+def augment_normalize(images, plans, size, mean=IMAGENET_MEAN, std=IMAGENET_STD, dtype=torch.float32):
+    """Device HWC uint8 images + their sampled plans -> [B, 3, H, W] augmented, resized, normalised
+    batch in one launch (yms_augment_normalize)."""
+    if not images or len(images) != len(plans):
+        raise ValueError("yms: one augmentation plan per image")
+    dev = images[0].device
+    if dev.type != "cuda":
+        raise RuntimeError("yms: augment_normalize runs on ROCm GPU tensors only (no CPU fallback)")
+    if L.lib().yms_augment_image_bytes() != ctypes.sizeof(AugImage):
+        raise RuntimeError("yms: AugImage layout differs from the library's")
+    H, W = size
+    n = len(images)
+    tab = (AugImage * n)()
+    for i, (im, pl) in enumerate(zip(images, plans)):
+        if im.device != dev or im.dtype != torch.uint8 or im.dim() != 3 or im.shape[2] != 3 or im.stride(2) != 1 \
+                or im.stride(1) != 3:
+            raise ValueError("yms: images must be contiguous HWC uint8 RGB tensors on one device")
+        if pl.frame != (W, H):
+            raise ValueError("yms: plan's final Resize does not produce the batch size")
+        tab[i] = plan_struct(pl, im)
+    tab_dev = torch.frombuffer(bytearray(tab), dtype=torch.uint8).to(dev, non_blocking=False)
+    out = torch.empty((n, 3, H, W), dtype=dtype, device=dev)
+    L.call("yms_augment_normalize", L.dtype_code(dtype), n, tab_dev.data_ptr(), H, W,
+           (ctypes.c_float * 3)(*mean), (ctypes.c_float * 3)(*std), out.data_ptr(), L.stream_ptr(dev))
+    for im in images:
+        im.record_stream(torch.cuda.current_stream(dev))
+    tab_dev.record_stream(torch.cuda.current_stream(dev))
+    return out
+
+
+def transform_boxes(boxes, labels, plan, min_visibility=0.1, min_area=1.0):
+    """COCO [x, y, w, h] pixel boxes of the plan's source image -> [n, 5] targets (class, cx, cy, w, h
+    normalised to the final frame).  Each box's corners go through every stage (continuous pixel
+    coordinates, X = index + 0.5); the box is the envelope of its transformed corners, clipped to
+    the final frame once; BboxParams(min_visibility=0.1, min_area=1) then drop boxes whose clipped
+    area is below 10% of the unclipped one or below 1 px, and the reference's final checks apply
+    (dataset.py:84-88, :218-228)."""
+    out_w, out_h = plan.frame
+    rows = []
+    for (x, y, w, h), c in zip(boxes, labels):
+        P = np.array([[x, y], [x + w, y], [x + w, y + h], [x, y + h]], np.float64) - 0.5
+        for F, *_ in plan.stages:
+            q = np.c_[P, np.ones(4)] @ F.T
+            P = q[:, :2] / q[:, 2:3]
+        P = P + 0.5
+        x0, y0 = P.min(0)
+        x1, y1 = P.max(0)
+        area = (x1 - x0) * (y1 - y0)
+        cx0, cy0 = min(max(x0, 0.0), out_w), min(max(y0, 0.0), out_h)
+        cx1, cy1 = min(max(x1, 0.0), out_w), min(max(y1, 0.0), out_h)
+        carea = max(cx1 - cx0, 0.0) * max(cy1 - cy0, 0.0)
+        if area <= 0 or carea / area < min_visibility or carea < min_area:
+            continue
+        bw, bh = cx1 - cx0, cy1 - cy0
+        cxn, cyn, wn, hn = (cx0 + bw / 2) / out_w, (cy0 + bh / 2) / out_h, bw / out_w, bh / out_h
+        if wn > 1e-3 and hn > 1e-3 and 0 <= cxn <= 1 and 0 <= cyn <= 1 and 0 <= wn <= 1 and 0 <= hn <= 1:
+            rows.append([c, cxn, cyn, wn, hn])
+    return torch.tensor(rows, dtype=torch.float32) if rows else torch.empty(0, 5)
 
 
 def flip_targets(t, flags):
@@ -182,8 +397,38 @@ class COCODetection(torch.utils.data.Dataset):
         return collate_targets(batch)
 
 
+class COCODataset(COCODetection):
+    """dataset.py:12-233 ``COCODataset(images_dir, annotations_file, transform_params=None,
+    is_train=True, img_size=(640, 640), num_classes=80)``: the training transform of
+    ``transform_params`` (the config's ``augmentation`` dict) is sampled per sample on the host
+    (``sample_augmentation``) and applied on the GPU by the collate (``collate_to_gpu``);
+    ``is_train=False`` keeps only the Resize.  ``__getitem__`` -> (decoded HWC uint8 image,
+    [n, 5] targets in the augmented frame, AugPlan)."""
+
+    def __init__(self, images_dir, annotations_file, transform_params=None, is_train=True, img_size=(640, 640),
+                 num_classes=80, seed=0):
+        super().__init__(images_dir, annotations_file, img_size=img_size, num_classes=num_classes, seed=seed)
+        self.transform_params = dict(transform_params or {})
+        self.is_train = is_train
+
+    def __getitem__(self, idx):
+        from PIL import Image
+        if torch.is_tensor(idx):
+            idx = idx.item()
+        if not isinstance(idx, int):
+            raise TypeError(f"Index should be an integer, got {type(idx).__name__} instead.")
+        info = self.imgs[self.image_ids[idx]]
+        image = np.array(Image.open(os.path.join(self.images_dir, info["file_name"])).convert("RGB"))
+        boxes, labels = self.annotations(idx)
+        h0, w0 = image.shape[:2]
+        plan = sample_augmentation(self.sample_rng(idx), self.transform_params, h0, w0, self.img_h, self.img_w,
+                                   self.is_train)
+        return image, transform_boxes(boxes, labels, plan), plan
+
+
 def collate_targets(batch):
-    """[(image, [n, 5] targets, flags)] -> (images, flags, [M, 6] targets with the batch index first)."""
+    """[(image, [n, 5] targets, flags or AugPlan)] -> (images, flags / plans, [M, 6] targets with the
+    batch index first)."""
     images, flags, rows = [], [], []
     for i, (img, t, f) in enumerate(batch):
         images.append(img)
@@ -196,7 +441,10 @@ def collate_targets(batch):
 
 def collate_to_gpu(batch, img_size, device, dtype=torch.float32, mean=IMAGENET_MEAN, std=IMAGENET_STD):
     """dataset.py collate_fn output on the GPU: ([B, 3, H, W] normalised images, [M, 6] targets)."""
-    images, flags, targets = collate_targets(batch)
+    images, extra, targets = collate_targets(batch)
     dev_images = to_device(images, device)
-    x = resize_normalize(dev_images, img_size, mean, std, flags, dtype)
+    if extra and isinstance(extra[0], AugPlan):
+        x = augment_normalize(dev_images, extra, img_size, mean, std, dtype)
+    else:
+        x = resize_normalize(dev_images, img_size, mean, std, extra, dtype)
     return x, targets.to(device, non_blocking=True)
