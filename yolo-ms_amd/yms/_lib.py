@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (loads the process' HIP runtime first)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libyms.so")
+LIB_PATH = os.environ.get("YMS_LIB") or os.path.join(_HERE, "libyms.so")   # YMS_LIB: dev A/B builds (tools/ab_lib.sh)
 
 F32, BF16, F16 = 0, 1, 2
 ACT_NONE, ACT_SILU = 0, 1
