@@ -279,3 +279,43 @@ def test_wgrad_3x3_halo(shp, dt, mode, monkeypatch):
         got = dw.double().cpu() - (0.25 if acc else 0.0)
         rel = ((got - ref).norm() / ref.norm()).item()
         assert rel < 1e-5 and (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, (acc, rel)
+
+
+# LDS-DMA ring weight gradient (wgrad_ring.hip): 1x1 and 3x3, stride 1 / 2, 64- and 128-row tiles
+# (cout 48, 64, 80, 128, 130, 256), 64-column GEMMs (1x1 with cin <= 64 on 128-row tiles), cin
+# not a multiple of 64 (40, 96, 200), pixel counts not a multiple of the k-tile, many splits,
+# channel slots of wider buffers; every ring variant (KP 64 / ST 2, KP 32 / ST 4, KP 64 / ST 3)
+WGR = [
+    (2, 64, 40, 40, 128, 3, 1), (3, 40, 13, 27, 48, 3, 1), (2, 96, 20, 20, 80, 1, 1), (1, 200, 17, 19, 130, 1, 1),
+    (2, 32, 33, 41, 256, 3, 2), (2, 64, 24, 24, 64, 1, 1), (4, 128, 20, 20, 256, 3, 1), (2, 48, 9, 5, 96, 3, 2),
+    (8, 128, 40, 40, 128, 1, 1), (1, 16, 7, 300, 72, 3, 1), (2, 256, 10, 10, 512, 3, 2),
+]
+
+
+@pytest.mark.parametrize("var", ["0", "1", "2", "3"])
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("shp", WGR)
+def test_wgrad_ring(shp, dt, var, monkeypatch):
+    monkeypatch.setenv("YMS_WG_HALO", "0")
+    monkeypatch.setenv("YMS_WG_RING", "2")
+    monkeypatch.setenv("YMS_WG_RING_VAR", var)
+    n, cin, h, w, cout, k, s = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(n * 7919 + cin * 31 + h + w + cout + s + k)
+    x = torch.randn(n, cin, h, w, generator=g)
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    dz = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+    xr, dzr = x.to(dtype).double(), dz.to(dtype).double()
+    ref = torch.nn.grad.conv2d_weight(xr, (cout, cin, k, k), dzr, stride=s, padding=k // 2)
+    sp = ctypes.pointer(shp_)
+    xb = nhwc(x, dtype, ld=r8(cin) + 16, off=8)
+    dzb = nhwc(dz, dtype, ld=r8(cout) + 16, off=16)
+    wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
+    ws = torch.full((wsb // 4 + 1,), float("nan"), dtype=torch.float32, device="cuda")
+    for acc in (0, 1):
+        dw = torch.full((cout, cin, k, k), 0.25, device="cuda")
+        L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 8, dzb.data_ptr(), dzb.shape[-1], 16,
+               ws.data_ptr(), wsb, dw.data_ptr(), acc, L.stream_ptr())
+        got = dw.double().cpu() - (0.25 if acc else 0.0)
+        rel = ((got - ref).norm() / ref.norm()).item()
+        assert rel < 1e-5 and (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, (acc, rel)

@@ -19,6 +19,7 @@
 #include "conv_common.hpp"
 #include "conv_halo.hpp"
 #include "wgrad_halo.hpp"
+#include "wgrad_ring.hpp"
 
 namespace yms {
 
@@ -1639,6 +1640,8 @@ size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
   WHPlan wh;
   if (wgrad_halo_plan(s, &wh)) return (size_t)wh.splits * wh.wk * wh.slab_rows * wh.slab_ld * sizeof(float);
+  WRPlan wr;
+  if (wgrad_ring_plan(s, &wr)) return (size_t)wr.splits * wr.slab_rows * wr.slab_ld * sizeof(float);
   WgradPlan w = wgrad_plan(s);
   return (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float);
 }
@@ -1660,6 +1663,20 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
       dim3 g2((unsigned)(s->cout * cdiv(kf, 128)));
       hipLaunchKernelGGL(wgrad_reduce_kernel, g2, dim3(256), 0, (hipStream_t)stream, ws, wh.splits * wh.wk,
                          (long)wh.slab_rows * wh.slab_ld, wh.slab_ld, s->cout, s->cin, cin8, s->k, dw, accumulate);
+      return launch_status();
+    }
+  }
+  {
+    // 1x1 / 3x3 with > 32 output channels: both operands on an LDS-DMA ring (wgrad_ring.hip)
+    WRPlan wr;
+    if (wgrad_ring_plan(s, &wr)) {
+      if (ws_bytes < (size_t)wr.splits * wr.slab_rows * wr.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
+      yms_status e = wgrad_ring_launch(s, wr, x, x_ld, x_off, dz, dz_ld, dz_off, ws, (hipStream_t)stream);
+      if (e != YMS_OK) return e;
+      const int kf = s->k * s->k * wr.cin8;
+      dim3 g2((unsigned)(s->cout * cdiv(kf, 128)));
+      hipLaunchKernelGGL(wgrad_reduce_kernel, g2, dim3(256), 0, (hipStream_t)stream, ws, wr.splits,
+                         (long)wr.slab_rows * wr.slab_ld, wr.slab_ld, s->cout, s->cin, wr.cin8, s->k, dw, accumulate);
       return launch_status();
     }
   }
