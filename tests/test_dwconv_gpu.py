@@ -15,7 +15,7 @@ from yms import _lib as L
 pytestmark = pytest.mark.gpu
 
 SHAPES = [(2, 20, 20, 64, 3), (1, 17, 33, 48, 5), (3, 40, 40, 32, 7), (2, 13, 9, 16, 9), (1, 80, 80, 64, 9),
-          (2, 8, 70, 40, 5)]
+          (2, 8, 70, 40, 5), (2, 24, 80, 32, 3), (2, 11, 45, 24, 7), (2, 40, 40, 128, 3), (1, 9, 23, 192, 3)]
 TOL = {"f32": 2e-5, "bf16": 1e-2}
 
 
@@ -25,9 +25,16 @@ def _close(got, ref, tol):
     assert err <= tol * scale + 1e-6, f"max err {err:.3g} vs scale {scale:.3g} (tol {tol})"
 
 
+# tile width of the forward / dgrad kernels: automatic (32 / 40 / 20 by the map width) or forced,
+# with the end-of-tile wait that leaves the tile's stores in flight (default) or drains them ("w"),
+# and 64-channel blocks for k = 3 (automatic when C % 64 == 0) or forced 32-channel blocks ("g4")
+@pytest.mark.parametrize("tx", ["0", "32", "40", "20", "0w", "0g4", "40g4"])
 @pytest.mark.parametrize("dt", ["f32", "bf16"])
 @pytest.mark.parametrize("shp", SHAPES)
-def test_dwconv_fwd_dgrad_wgrad(shp, dt):
+def test_dwconv_fwd_dgrad_wgrad(shp, dt, tx, monkeypatch):
+    monkeypatch.setenv("YMS_DW_TX", tx.replace("g4", "").rstrip("w"))
+    monkeypatch.setenv("YMS_DW_WAITALL", "1" if tx.endswith("w") else "0")
+    monkeypatch.setenv("YMS_DW_G", "4" if tx.endswith("g4") else "0")
     n, h, w, c, k = shp
     dtype = DT[dt]
     g = torch.Generator().manual_seed(sum(shp))

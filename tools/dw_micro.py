@@ -10,8 +10,20 @@ SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64
           (64, 80, 80, 64, 3), (64, 40, 40, 128, 3)]
 if os.environ.get("YMS_MICRO_SHAPES") == "k9":
     SHAPES = [(64, 20, 20, 512, 9)]
-if os.environ.get("YMS_MICRO_SHAPES") == "mss":   # YOLO-MS-S depthwise layers at B=64
-    SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 384, 3), (64, 40, 40, 768, 3), (64, 20, 20, 512, 3)]
+if os.environ.get("YMS_MICRO_SHAPES") == "mss":   # YOLO-MS-S depthwise layers at B=64 (x2, x2, x2, x2, x4, x4)
+    SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9),
+              (64, 80, 80, 384, 3), (64, 40, 40, 768, 3)]
+# env variants timed side by side (each read per call): name=VAR:VAL,VAR:VAL;...
+VARIANTS = [("default", {})]
+if os.environ.get("YMS_DWM_VARIANTS"):
+    VARIANTS = []
+    for item in os.environ["YMS_DWM_VARIANTS"].split(";"):
+        name, _, kv = item.partition("=")
+        VARIANTS.append((name, dict(p.split(":") for p in kv.split(",") if p)))
+if os.environ.get("YMS_DWM_OPS"):
+    OPS = os.environ["YMS_DWM_OPS"].split(",")
+else:
+    OPS = None
 for (n, h, w, c, k) in SHAPES:
     sh = L.DwShape(n, h, w, c, k, L.BF16)
     sp = ctypes.pointer(sh)
@@ -38,13 +50,22 @@ for (n, h, w, c, k) in SHAPES:
     }
     nb = x.numel() * 2 * 2
     for name, fn in ops.items():
-        for _ in range(3):
-            fn()
-        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        s.record()
-        for _ in range(10):
-            fn()
-        e.record()
-        torch.cuda.synchronize()
-        us = s.elapsed_time(e) * 100
-        print(f"{name:9s} {n}x{h}x{w} c{c} k{k}: {us:8.1f} us  {nb / us / 1e3:7.0f} GB/s", flush=True)
+        if OPS and name not in OPS:
+            continue
+        line = f"{name:9s} {n}x{h}x{w} c{c} k{k}:"
+        for vname, env in VARIANTS:
+            for a, b in env.items():
+                os.environ[a] = b
+            for _ in range(3):
+                fn()
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                fn()
+            e.record()
+            torch.cuda.synchronize()
+            us = s.elapsed_time(e) * 100
+            line += f"  {vname} {us:7.1f} us {nb / us / 1e3:5.0f} GB/s"
+            for a in env:
+                os.environ.pop(a, None)
+        print(line, flush=True)

@@ -42,6 +42,7 @@ struct DwParams {
   int N, H, W, C;
   int tiles_x, tiles_y;  // spatial tiles per image
   int ysplit, tps;       // forward / dgrad: strips per image column of tiles, tiles per strip
+  int waitall;
 };
 
 // LDS row stride (16-B chunks) for rows of n chunks: one chunk of padding when n is a multiple
@@ -78,10 +79,10 @@ typedef int i32x4 __attribute__((ext_vector_type(4)));
 // the current tile (the ring slots written and read are disjoint by construction); completion is
 // counted by hand (wait_vmcnt<0> + barrier at the end of each tile).  M0 is saved and restored in
 // the same statement (it is compiler-reserved).
-template <typename T, int K>
+template <typename T, int K, int TX = DW_TX>
 __device__ __forceinline__ void dw_row_dma(i32x4 rs, uint32_t lds_row, int y, int x0, int c, int H, int W, int C,
                                            int ld, int lane) {
-  constexpr int CPE = (int)sizeof(T) / 2, NCH = (DW_TX + K - 1) * CPE;
+  constexpr int CPE = (int)sizeof(T) / 2, NCH = (TX + K - 1) * CPE;
 #pragma unroll
   for (int j0 = 0; j0 < NCH; j0 += 64) {
     const int j = j0 + lane;
@@ -113,15 +114,49 @@ template <typename T, int K> struct DwOcc {
   static constexpr int v = sizeof(T) == 4 ? (K == 3 ? 2 : 1) : (K == 3 ? 4 : (K == 5 ? 3 : 2));
 };
 
-template <typename T, int K, int MODE>
-__global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams p) {
-  constexpr int P = K / 2, HW = DW_TX + K - 1, RB = 2 * DW_TY + K - 1;
+// forward / dgrad tile widths: TX = 32 (8 rows), 40 (6 rows) or 20 (12 rows) output pixels, RX = 4
+// per lane, so the lanes of a wave cover TY rows x TX / 4 column groups (64 / 60 / 60 lanes) and a
+// 20-, 40- or 80-wide map wastes no columns (a 32-wide tile used 62.5 % of its lanes at 40^2 and
+// 52 % at 20^2, where the k = 7 / 9 layers of the MS-Blocks sit)
+template <int TX> struct DwTy { static constexpr int v = TX == 32 ? 8 : (TX == 40 ? 6 : 12); };
+
+// raw-buffer 16-B store; an offset at or past num_records is dropped by the hardware, so every
+// lane of every wave issues the same store instructions (the end-of-tile wait counts them)
+__device__ __forceinline__ void dw_bst16(__amdgpu_buffer_rsrc_t rs, uint32_t voff, const u32x4& v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_buffer_store_b128(v, rs, voff, 0, 0);
+#else
+  (void)rs; (void)voff; (void)v;
+#endif
+}
+__device__ __forceinline__ void dw_bst4(__amdgpu_buffer_rsrc_t rs, uint32_t voff, float v) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v), rs, voff, 0, 0);
+#else
+  (void)rs; (void)voff; (void)v;
+#endif
+}
+template <typename T>
+__device__ __forceinline__ Raw8<T> pack_raw8(const float (&v)[8]) {
+  T t[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) t[i] = (T)v[i];
+  Raw8<T> r;
+  __builtin_memcpy(&r, t, sizeof(t));
+  return r;
+}
+
+template <typename T, int K, int MODE, int TX = DW_TX, int G = DW_G>
+__global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_kernel(DwParams p) {
+  constexpr int CB = G * 8, NT = G * 64;
+  constexpr int TY = DwTy<TX>::v, CGX = TX / DW_RX;
+  constexpr int P = K / 2, HW = TX + K - 1, RB = 2 * TY + K - 1;
   // ONE __shared__ object: a second one beside the LDS-DMA target makes hipcc wait vmcnt(0) before
   // the first ds_read of every kernel row (cdna_hip_programming.md, .s-level trap (a))
   constexpr int RS = dw_rs(HW);   // ring row stride (chunks)
-  constexpr int RING_B = DW_G * RB * RS * (int)sizeof(Raw8<T>);
-  constexpr int WL_B = DW_G * K * K * 8 * (int)sizeof(float);
-  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + DW_G * 16 * (int)sizeof(float)];
+  constexpr int RING_B = G * RB * RS * (int)sizeof(Raw8<T>);
+  constexpr int WL_B = G * K * K * 8 * (int)sizeof(float);
+  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + G * 16 * (int)sizeof(float)];
   Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
   float (*wl)[K * K][8] = reinterpret_cast<float (*)[K * K][8]>(smem + RING_B);
   float (*scl)[16] = reinterpret_cast<float (*)[16]>(smem + RING_B + WL_B);   // eval scale | shift (LDS:
@@ -129,36 +164,36 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
   const int per_img = p.tiles_x * p.ysplit;
   const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
   const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
-  const int x0 = tx * DW_TX;
-  const int c0 = blockIdx.y * DW_CB;
+  const int x0 = tx * TX;
+  const int c0 = blockIdx.y * CB;
   {
     // the block's 32 x K x K weights are one contiguous range of p.w: coalesced loads, all issued
     // before the LDS stores (dgrad correlates with the kernel rotated by 180 degrees)
-    constexpr int NWL = (DW_CB * K * K + 255) / 256;
-    const int nvalid = min(DW_CB, p.C - c0) * K * K;
+    constexpr int NWL = (CB * K * K + NT - 1) / NT;
+    const int nvalid = min(CB, p.C - c0) * K * K;
     float wv[NWL];
 #pragma unroll
     for (int j = 0; j < NWL; ++j) {
-      const int it = threadIdx.x + 256 * j;
+      const int it = threadIdx.x + NT * j;
       wv[j] = it < nvalid ? p.w[(long)c0 * K * K + it] : 0.0f;
     }
 #pragma unroll
     for (int j = 0; j < NWL; ++j) {
-      const int it = threadIdx.x + 256 * j;
-      if (it < DW_CB * K * K) {
+      const int it = threadIdx.x + NT * j;
+      if (it < CB * K * K) {
         const int cl = it / (K * K), t = it - cl * (K * K);
         const int tw = MODE == DW_DGRAD ? K * K - 1 - t : t;
         wl[cl >> 3][tw][cl & 7] = wv[j];
       }
     }
   }
-  if (MODE == DW_FWD_AFFINE && threadIdx.x < DW_G * 16) {
+  if (MODE == DW_FWD_AFFINE && threadIdx.x < G * 16) {
     const int gg = threadIdx.x >> 4, k = threadIdx.x & 7, c = c0 + 8 * gg + k;
     scl[gg][threadIdx.x & 15] = (threadIdx.x & 8) ? ((p.shift && c < p.C) ? p.shift[c] : 0.0f)
                                                   : ((p.scale && c < p.C) ? p.scale[c] : 1.0f);
   }
   const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int ty = lane >> 3, qx = lane & 7;
+  const int ty = lane / CGX, qx = lane - ty * CGX;   // ty >= TY: idle lane (60 of 64 used at TX 20 / 40)
   const int c = c0 + 8 * g, nv = min(8, p.C - c);
   // raw buffer resource over image n's rows (32-bit offsets: checked on the host)
   const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
@@ -168,24 +203,35 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
   const uint32_t myring = __builtin_amdgcn_readfirstlane(
       (uint32_t)reinterpret_cast<uintptr_t>(ring + g * RB * RS));   // LDS byte address (wave-uniform)
   constexpr uint32_t ROWB = RS * (uint32_t)sizeof(Raw8<T>);
+  // destination resource over image n (32-bit offsets, checked on the host); stores go through it
+  // so every wave issues the same, unconditional store instructions (out-of-tile lanes: NT_OOB)
+  const uintptr_t db = reinterpret_cast<uintptr_t>(reinterpret_cast<T*>(p.dst) + (long)n * p.H * p.W * p.dst_ld +
+                                                   p.dst_off);
+  const __amdgpu_buffer_rsrc_t rd = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)db, (short)0, (int)((long)p.H * p.W * p.dst_ld * (long)sizeof(T)), NT_RSRC3);
+  const long srows = (long)p.N * p.tiles_y * p.tiles_x;
+  const __amdgpu_buffer_rsrc_t rstat = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.stats, (short)0, MODE == DW_FWD_STATS ? (int)(srows * 2 * p.stats_ld * 4) : 0, NT_RSRC3);
+  const __amdgpu_buffer_rsrc_t rcnt = __builtin_amdgcn_make_buffer_rsrc(
+      (void*)p.stats_cnt, (short)0, MODE == DW_FWD_STATS ? (int)(srows * 4) : 0, NT_RSRC3);
   // prologue: the first tile's TY + K - 1 rows
-  for (int hy = 0; hy < DW_TY + K - 1; ++hy)
-    dw_row_dma<T, K>(rs, myring + ((t0 * DW_TY + hy) % RB) * ROWB, t0 * DW_TY - P + hy, x0, c, p.H, p.W, p.C,
-                     p.src_ld, lane);
+  for (int hy = 0; hy < TY + K - 1; ++hy)
+    dw_row_dma<T, K, TX>(rs, myring + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
+                         p.src_ld, lane);
   wait_vmcnt<0>();
   __syncthreads();
   for (int t = t0; t < t1; ++t) {
-    const int y0 = t * DW_TY;
+    const int y0 = t * TY;
     const bool more = t + 1 < t1;
     // the next tile's TY new rows y0 + TY + P .. y0 + 2 TY - 1 + P go to slots this tile does not read
     if (more) {
-      int sl = (y0 + DW_TY + 2 * P) % RB;
-      for (int hy = 0; hy < DW_TY; ++hy) {
-        dw_row_dma<T, K>(rs, myring + sl * ROWB, y0 + DW_TY + P + hy, x0, c, p.H, p.W, p.C, p.src_ld, lane);
+      int sl = (y0 + TY + 2 * P) % RB;
+      for (int hy = 0; hy < TY; ++hy) {
+        dw_row_dma<T, K, TX>(rs, myring + sl * ROWB, y0 + TY + P + hy, x0, c, p.H, p.W, p.C, p.src_ld, lane);
         sl = sl + 1 == RB ? 0 : sl + 1;
       }
     }
-    const Raw8<T>* hp = ring + g * RB * RS + 4 * qx;
+    const Raw8<T>* hp = ring + g * RB * RS + 4 * (ty < TY ? qx : 0);
     float acc[DW_RX][8];
 #pragma unroll
     for (int i = 0; i < DW_RX; ++i)
@@ -221,43 +267,49 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
     }
     const int tile = (n * p.tiles_y + t) * p.tiles_x + tx;   // statistics row (image-major tiles)
     const int y = y0 + ty;
-    if (nv > 0 && y < p.H) {
-      T* dst = reinterpret_cast<T*>(p.dst);
+    const bool yok = ty < TY && y < p.H;
+    // every wave issues exactly NST vector-memory instructions after its last DMA of this tile (the
+    // stores below; statistics: two row stores and the count): the end-of-tile wait leaves them in
+    // flight and waits for the next tile's rows only (vmcnt retires in issue order on gfx9)
+    constexpr int NST = DW_RX * (int)(sizeof(T) / 2) + (MODE == DW_FWD_STATS ? 3 : 0);
 #pragma unroll
-      for (int i = 0; i < DW_RX; ++i) {
-        const int x = x0 + 4 * qx + i;
-        if (x >= p.W) continue;
-        float o[8];
+    for (int i = 0; i < DW_RX; ++i) {
+      const int x = x0 + 4 * qx + i;
+      const bool ok = nv > 0 && yok && x < p.W;
+      float o[8];
 #pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          float v = acc[i][k];
-          if (MODE == DW_FWD_AFFINE) {
-            v = v * scl[g][k] + scl[g][8 + k];
-            if (p.act == YMS_ACT_SILU) v = silu_f(v);
-          }
-          o[k] = v;
+      for (int k = 0; k < 8; ++k) {
+        float v = acc[i][k];
+        if (MODE == DW_FWD_AFFINE) {
+          v = v * scl[g][k] + scl[g][8 + k];
+          if (p.act == YMS_ACT_SILU) v = silu_f(v);
         }
-        T* d = dst + (((long)n * p.H + y) * p.W + x) * p.dst_ld + p.dst_off + c;
-        if (MODE == DW_DGRAD && p.accumulate) {
-          float r[8];
-          load8(d, nv, r);
-#pragma unroll
-          for (int k = 0; k < 8; ++k) o[k] += r[k];
-        }
-        store8(d, nv, o);
+        o[k] = v;
       }
+      const uint32_t e = ok ? (uint32_t)((y * p.W + x) * p.dst_ld + c) : 0u;
+      if (MODE == DW_DGRAD && p.accumulate) {
+        // (this load retires the tile's DMA with it: accumulation is the rare case)
+        float r[8];
+        if (ok) load8(reinterpret_cast<const T*>(db) + e, nv, r);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) o[k] += ok ? r[k] : 0.0f;
+      }
+      const Raw8<T> rv = pack_raw8<T>(o);
+#pragma unroll
+      for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
+        dw_bst16(rd, ok ? e * (uint32_t)sizeof(T) + 16u * h : NT_OOB, rv.v[h]);
     }
     if (MODE == DW_FWD_STATS) {
       // one statistics row per spatial tile (conv_common.hpp contract; its pixel count goes to the
       // count table after the rows): sum and centred M2 over the tile's valid pixels, two passes
       // over the fp32 accumulators, wave butterflies in a fixed order
-      const int vy = min(DW_TY, p.H - y0), vx = min(DW_TX, p.W - x0);
+      const int vy = min(TY, p.H - y0), vx = min(TX, p.W - x0);
       const float inv_n = 1.0f / (float)(vy * vx);
       float s1[8], m2[8];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         float s = 0.f;
-        if (y < p.H) {
+        if (yok) {
 #pragma unroll
           for (int i = 0; i < DW_RX; ++i)
             if (x0 + 4 * qx + i < p.W) s += acc[i][k];
@@ -266,7 +318,7 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
         for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
         const float mu = s * inv_n;
         float q = 0.f;
-        if (y < p.H) {
+        if (yok) {
 #pragma unroll
           for (int i = 0; i < DW_RX; ++i)
             if (x0 + 4 * qx + i < p.W) {
@@ -279,18 +331,18 @@ __global__ __launch_bounds__(256, (DwOcc<T, K>::v)) void dwconv_kernel(DwParams 
         s1[k] = s;
         m2[k] = q;
       }
-      if (lane < 8 && c + lane < p.C) {
-        float a = 0.f, b = 0.f;
+      float a = 0.f, b = 0.f;
 #pragma unroll
-        for (int k = 0; k < 8; ++k)
-          if (k == lane) { a = s1[k]; b = m2[k]; }
-        float* so = p.stats + (long)tile * 2 * p.stats_ld;
-        so[c + lane] = a;
-        so[p.stats_ld + c + lane] = b;
-      }
-      if (blockIdx.y == 0 && threadIdx.x == 0) p.stats_cnt[tile] = (float)(vy * vx);
+      for (int k = 0; k < 8; ++k)
+        if (k == lane) { a = s1[k]; b = m2[k]; }
+      const bool sok = lane < 8 && c + lane < p.C;
+      const uint32_t so = (uint32_t)(((long)tile * 2 * p.stats_ld + c + lane) * 4);
+      dw_bst4(rstat, sok ? so : NT_OOB, a);
+      dw_bst4(rstat, sok ? so + (uint32_t)p.stats_ld * 4u : NT_OOB, b);
+      dw_bst4(rcnt, (blockIdx.y == 0 && threadIdx.x == 0) ? (uint32_t)tile * 4u : NT_OOB, (float)(vy * vx));
     }
-    wait_vmcnt<0>();
+    if (!p.waitall) wait_vmcnt<NST>();
+    else wait_vmcnt<0>();   // dev A/B (YMS_DW_WAITALL=1): also drain the tile's stores
     __syncthreads();
   }
 }
@@ -441,16 +493,70 @@ static int dw_tiles(const yms_dw_shape* s, int& tx, int& ty) {
   return s->n * tx * ty;
 }
 
-// forward / dgrad grid: image column tiles split into strips of tps tiles; strips are split only
-// as far as needed for about 2048 blocks (8 per CU), longer strips re-read fewer halo rows
+static int dw_env(const char* name, int dflt) {
+  const char* v = getenv(name);
+  return v ? atoi(v) : dflt;
+}
+// forward / dgrad tile width (DwTy): whole tiles across the 20 / 40 / 80-wide maps of a 640 input,
+// 32 where it divides the width (YMS_DW_TX=32|40|20 forces one: dev A/B, read per call)
+static int dw_fwd_tx(const yms_dw_shape* s) {
+  const int f = dw_env("YMS_DW_TX", 0);
+  if (f == 32 || f == 40 || f == 20) return f;
+  if (s->w % 32 == 0) return 32;
+  if (s->w % 40 == 0) return 40;
+  if (s->w <= 20) return 20;
+  if (s->w <= 40) return 40;
+  return 32;
+}
+static int dw_fwd_ty(int tx) { return tx == 32 ? 8 : (tx == 40 ? 6 : 12); }
+static int dw_fwd_tiles(const yms_dw_shape* s, int& tx, int& ty) {
+  const int TX = dw_fwd_tx(s), TY = dw_fwd_ty(TX);
+  tx = (s->w + TX - 1) / TX;
+  ty = (s->h + TY - 1) / TY;
+  return s->n * tx * ty;
+}
+static int dw_occ(const yms_dw_shape* s) {
+  if (s->dtype == YMS_F32) return s->k == 3 ? 2 : 1;
+  return s->k == 3 ? 4 : (s->k == 5 ? 3 : 2);
+}
+
+// channel groups of 8 per forward / dgrad block: 8 (64 channels = one 128-B line of an NHWC pixel
+// per block, 512 threads) for k = 3 when C is a multiple of 64, else 4 (32 channels: the other half
+// of each line is read and written by another block at another time).  YMS_DW_G=4|8 forces (dev A/B).
+static int dw_fwd_g(const yms_dw_shape* s) {
+  const int f = dw_env("YMS_DW_G", 0);
+  if ((f == 4 || f == 8) && (f == 4 || s->k == 3)) return f;
+  return (s->k == 3 && s->c % 64 == 0 && s->dtype != YMS_F32) ? 8 : 4;
+}
+
+// forward / dgrad grid: image column tiles split into strips of tps tiles.  The strip length is
+// chosen so the blocks fill whole rounds of the resident slots (occupancy x CUs): a block walks its
+// strip serially, so a last round of a few blocks costs a full strip time, while shorter strips
+// re-read K - 1 halo rows each (cost model: rounds x (tps TY + K - 1) rows).  YMS_DW_BLOCKS=n
+// restores the earlier rule (strips split until about n blocks).
 static dim3 dw_strip_grid(const yms_dw_shape* s, DwParams& p) {
-  dw_tiles(s, p.tiles_x, p.tiles_y);
-  const long cg = (s->c + DW_CB - 1) / DW_CB;
+  dw_fwd_tiles(s, p.tiles_x, p.tiles_y);
+  const int TY = dw_fwd_ty(dw_fwd_tx(s)), G = dw_fwd_g(s);
+  const long cg = (s->c + 8 * G - 1) / (8 * G);
   const long base = (long)s->n * p.tiles_x * cg;
-  static const long target = getenv("YMS_DW_BLOCKS") ? std::max(1, atoi(getenv("YMS_DW_BLOCKS"))) : 2048;   // dev A/B
-  const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (target + base - 1) / base));
-  p.tps = (p.tiles_y + want - 1) / want;
+  const long target = dw_env("YMS_DW_BLOCKS", 0);
+  if (target > 0) {
+    const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (target + base - 1) / base));
+    p.tps = (p.tiles_y + want - 1) / want;
+  } else {
+    const long slots = (long)(G == 8 ? 2 : dw_occ(s)) * conv_cu_count();
+    double best = 1e30;
+    int best_tps = p.tiles_y;
+    for (int tps = p.tiles_y; tps >= 1; --tps) {
+      const long ys = (p.tiles_y + tps - 1) / tps;
+      const long rounds = (base * ys + slots - 1) / slots;
+      const double cost = (double)rounds * (tps * TY + s->k - 1);
+      if (cost < best * 0.999) { best = cost; best_tps = tps; }
+    }
+    p.tps = best_tps;
+  }
   p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
+  p.waitall = dw_env("YMS_DW_WAITALL", 0);
   return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
 }
 
@@ -482,6 +588,17 @@ static int dw_wgrad_blocks(const yms_dw_shape* s) {
     case 7: { constexpr int KK = 7; __VA_ARGS__; } break;       \
     default: { constexpr int KK = 9; __VA_ARGS__; } break;      \
   }
+#define YMS_DW_TXS(TXV, ...)                                    \
+  do {                                                          \
+    if ((TXV) == 40) { constexpr int TXX = 40; __VA_ARGS__; }   \
+    else if ((TXV) == 20) { constexpr int TXX = 20; __VA_ARGS__; } \
+    else { constexpr int TXX = 32; __VA_ARGS__; }               \
+  } while (0)
+#define YMS_DW_T16(dt, ...)                                     \
+  do {                                                          \
+    if ((dt) == YMS_BF16) { typedef bf16 TT; __VA_ARGS__; }     \
+    else { typedef f16 TT; __VA_ARGS__; }                       \
+  } while (0)
 #define YMS_DW_T(dt, ...)                                       \
   do {                                                          \
     if ((dt) == YMS_BF16) { typedef bf16 TT; __VA_ARGS__; }     \
@@ -539,7 +656,7 @@ extern "C" {
 int yms_dwconv_stats_rows(const yms_dw_shape* s) {
   if (!dw_shape_ok(s)) return 0;
   int tx, ty;
-  return dw_tiles(s, tx, ty);
+  return dw_fwd_tiles(s, tx, ty);
 }
 
 yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
@@ -548,7 +665,8 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   if (!dw_shape_ok(s) || !x || !w || !y || !dw_view_ok(x_ld, x_off, s->c) || !dw_view_ok(y_ld, y_off, s->c))
     return YMS_ERR_INVALID;
   if (stats && stats_ld < s->c) return YMS_ERR_INVALID;
-  if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
+  if (!dw_image_fits(s, x_ld) || !dw_image_fits(s, y_ld)) return YMS_ERR_UNSUPPORTED;
+  if (stats && (long)yms_dwconv_stats_rows(s) * 2 * stats_ld * 4 >= (long)NT_OOB) return YMS_ERR_UNSUPPORTED;
   DwParams p{};
   p.src = (const char*)x; p.src_ld = x_ld; p.src_off = x_off; p.w = w;
   p.dst = (char*)y; p.dst_ld = y_ld; p.dst_off = y_off;
@@ -557,10 +675,18 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
   const dim3 grid = dw_strip_grid(s, p);
   hipStream_t st = (hipStream_t)stream;
-  YMS_DW_T(s->dtype, YMS_DW_K(s->k, {
-    if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_STATS>), grid, dim3(256), 0, st, p);
-    else hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_AFFINE>), grid, dim3(256), 0, st, p);
-  }));
+  const int TX = dw_fwd_tx(s);
+  if (dw_fwd_g(s) == 8) {
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
+      if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_STATS, TXX, 8>), grid, dim3(512), 0, st, p);
+      else hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_AFFINE, TXX, 8>), grid, dim3(512), 0, st, p);
+    }));
+    return launch_status();
+  }
+  YMS_DW_T(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, {
+    if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_STATS, TXX>), grid, dim3(256), 0, st, p);
+    else hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_AFFINE, TXX>), grid, dim3(256), 0, st, p);
+  })));
   return launch_status();
 }
 
@@ -568,14 +694,21 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
                             int dx_ld, int dx_off, int accumulate, void* stream) {
   if (!dw_shape_ok(s) || !dz || !w || !dx || !dw_view_ok(dz_ld, dz_off, s->c) || !dw_view_ok(dx_ld, dx_off, s->c))
     return YMS_ERR_INVALID;
-  if (!dw_image_fits(s, dz_ld)) return YMS_ERR_UNSUPPORTED;
+  if (!dw_image_fits(s, dz_ld) || !dw_image_fits(s, dx_ld)) return YMS_ERR_UNSUPPORTED;
   DwParams p{};
   p.src = (const char*)dz; p.src_ld = dz_ld; p.src_off = dz_off; p.w = w;
   p.dst = (char*)dx; p.dst_ld = dx_ld; p.dst_off = dx_off; p.accumulate = accumulate;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
   const dim3 grid = dw_strip_grid(s, p);
   hipStream_t st = (hipStream_t)stream;
-  YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_DGRAD>), grid, dim3(256), 0, st, p)));
+  const int TX = dw_fwd_tx(s);
+  if (dw_fwd_g(s) == 8) {
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_DGRAD, TXX, 8>), grid, dim3(512), 0,
+                                                           st, p)));
+    return launch_status();
+  }
+  YMS_DW_T(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_DGRAD, TXX>), grid,
+                                                                     dim3(256), 0, st, p))));
   return launch_status();
 }
 
