@@ -149,7 +149,8 @@ def conv_roofline(prof, label):
 
 
 VALU_F32_PEAK_TFLOPS = 157.3    # fp32 vector FMA rate, MI355X_MICROARCH.md chip table
-DW_NAMES = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
+DW_NAMES = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_dgrad_bnred", "yms_dwconv_wgrad", "yms_dwconv_fwd_bnin",
+            "yms_dwconv_wgrad_bnin")
 BN_NAMES = ("yms_bn_act_bwd_reduce", "yms_bn_act_bwd_apply", "yms_affine_act", "yms_add_views", "yms_add_grad2")
 
 

@@ -24,7 +24,13 @@
 namespace yms {
 
 constexpr int DW_TY = 8, DW_TX = 32, DW_RX = 4, DW_G = 4, DW_CB = DW_G * 8;   // 32 channels per block
-enum { DW_FWD_AFFINE = 0, DW_FWD_STATS = 1, DW_DGRAD = 2 };
+// DW_DGRAD_RED: dgrad whose output (the producer's activation gradient, sole writer) also feeds
+// the producer's BN + SiLU backward statistics: the fused pass reads the producer's z once per
+// output pixel and writes one partial row per strip -- the separate reduce pass re-read dx and z
+// DW_FWD_STATS_BNIN: the training forward whose input x = act(BN(z)) of the producer is not
+// materialised: the producer's z rows land in the ring and are converted in LDS once per element
+// (zero padding stays zero) -- the producer's affine_act pass (read z, write x) goes
+enum { DW_FWD_AFFINE = 0, DW_FWD_STATS = 1, DW_DGRAD = 2, DW_DGRAD_RED = 3, DW_FWD_STATS_BNIN = 4 };
 
 struct DwParams {
   const char* src;
@@ -43,7 +49,56 @@ struct DwParams {
   int tiles_x, tiles_y;  // spatial tiles per image
   int ysplit, tps;       // forward / dgrad: strips per image column of tiles, tiles per strip
   int waitall;
+  // DW_DGRAD_RED: the producer's pre-BN z (same pixels / channels as dx), its BN scale / shift /
+  // (mean, invstd), activation, and the partial rows [strip][2][C] (bn_bwd_reduce_kernel layout)
+  const char* rz;
+  int rz_ld, rz_off;
+  const float *rsc, *rsh, *rmi;
+  int ract;
+  float* rws;
+  // DW_FWD_STATS_BNIN / wgrad with an input affine: x = act(src * isc + ish) per channel
+  const float *isc, *ish;
+  int iact;
 };
+
+// per-element input transform of a staged chunk (the producer's affine_act formula)
+template <typename T>
+__device__ __forceinline__ void dw_in_affine(Raw8<T>& r, const float (&sc)[8], const float (&sh)[8], int act) {
+  float v[8];
+  unpack8(r, v);
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float a = v[k] * sc[k] + sh[k];
+    if (act == YMS_ACT_SILU) a = silu_f(a);
+    v[k] = a;
+  }
+  T t[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) t[k] = (T)v[k];
+  __builtin_memcpy(&r, t, sizeof(t));
+}
+// convert rows [yfirst, yfirst + nrows) of a wave's ring in place (valid pixels only: the padding
+// the DMA zero-filled must stay zero, not act(shift)); wave-local, ends with the LDS writes done
+template <typename T, int K, int HW, int RB, int RS>
+__device__ __forceinline__ void dw_ring_in_affine(Raw8<T>* wring, int yfirst, int nrows, int x0, int H, int W,
+                                                  bool cok, const float (&sc)[8], const float (&sh)[8], int act,
+                                                  int lane) {
+  constexpr int P = K / 2;
+  if (cok) {
+    for (int j = lane; j < nrows * HW; j += 64) {
+      const int r = j / HW, col = j - r * HW;
+      const int y = yfirst + r, x = x0 - P + col;
+      if (y >= 0 && y < H && x >= 0 && x < W) {
+        Raw8<T>* cp = wring + ((y + P) % RB) * RS + col;
+        Raw8<T> v = *cp;
+        dw_in_affine<T>(v, sc, sh, act);
+        *cp = v;
+      }
+    }
+  }
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
+  __builtin_amdgcn_wave_barrier();
+}
 
 // LDS row stride (16-B chunks) for rows of n chunks: one chunk of padding when n is a multiple
 // of 4 (a 64-B multiple: rows read by one wave's lanes would start in the same banks); other
@@ -52,7 +107,7 @@ constexpr int dw_rs(int n) { return n % 4 == 0 ? n + 1 : n; }
 
 // stage the (TY + K - 1) x (TX + K - 1) halo of 32 channels (zero outside the image / past C)
 // into rows of dw_rs(HW) chunks
-template <typename T, int K, int NT = 256>
+template <typename T, int K, int NT = 256, bool BNIN = false>
 __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, int n, int y0, int x0, int c0) {
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1, P = K / 2, RS = dw_rs(HW);
   const T* src = reinterpret_cast<const T*>(p.src);
@@ -63,8 +118,18 @@ __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, i
     Raw8<T> v;
 #pragma unroll
     for (int k = 0; k < (int)(sizeof(T) / 2); ++k) v.v[k] = u32x4{0u, 0u, 0u, 0u};
-    if (y >= 0 && y < p.H && x >= 0 && x < p.W && c < p.C)
+    if (y >= 0 && y < p.H && x >= 0 && x < p.W && c < p.C) {
       load_raw8(src + (((long)n * p.H + y) * p.W + x) * p.src_ld + p.src_off + c, min(8, p.C - c), v);
+      if constexpr (BNIN) {
+        float sc[8], sh[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          sc[k] = c + k < p.C ? p.isc[c + k] : 0.f;
+          sh[k] = c + k < p.C ? p.ish[c + k] : 0.f;
+        }
+        dw_in_affine<T>(v, sc, sh, p.iact);
+      }
+    }
     lds[(g * HH + hy) * RS + hx] = v;
   }
 }
@@ -147,7 +212,8 @@ __device__ __forceinline__ Raw8<T> pack_raw8(const float (&v)[8]) {
 }
 
 template <typename T, int K, int MODE, int TX = DW_TX, int G = DW_G>
-__global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_kernel(DwParams p) {
+__global__ __launch_bounds__(G * 64, (MODE == 3 ? (G == 8 ? 1 : 2) : (G == 8 ? 2 : DwOcc<T, K>::v)))
+void dwconv_kernel(DwParams p) {
   constexpr int CB = G * 8, NT = G * 64;
   constexpr int TY = DwTy<TX>::v, CGX = TX / DW_RX;
   constexpr int P = K / 2, HW = TX + K - 1, RB = 2 * TY + K - 1;
@@ -156,7 +222,12 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
   constexpr int RS = dw_rs(HW);   // ring row stride (chunks)
   constexpr int RING_B = G * RB * RS * (int)sizeof(Raw8<T>);
   constexpr int WL_B = G * K * K * 8 * (int)sizeof(float);
-  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + G * 16 * (int)sizeof(float)];
+  constexpr bool RED = MODE == DW_DGRAD_RED;
+  constexpr bool BNIN = MODE == DW_FWD_STATS_BNIN;
+  constexpr bool STATS = MODE == DW_FWD_STATS || BNIN;
+  constexpr int RP_B = RED ? G * 4 * 8 * (int)sizeof(float) : 0;
+  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + G * 16 * (int)sizeof(float) + RP_B];
+  float (*rpar)[4][8] = reinterpret_cast<float (*)[4][8]>(smem + RING_B + WL_B + G * 16 * (int)sizeof(float));
   Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
   float (*wl)[K * K][8] = reinterpret_cast<float (*)[K * K][8]>(smem + RING_B);
   float (*scl)[16] = reinterpret_cast<float (*)[16]>(smem + RING_B + WL_B);   // eval scale | shift (LDS:
@@ -182,7 +253,7 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
       const int it = threadIdx.x + NT * j;
       if (it < CB * K * K) {
         const int cl = it / (K * K), t = it - cl * (K * K);
-        const int tw = MODE == DW_DGRAD ? K * K - 1 - t : t;
+        const int tw = (MODE == DW_DGRAD || MODE == DW_DGRAD_RED) ? K * K - 1 - t : t;
         wl[cl >> 3][tw][cl & 7] = wv[j];
       }
     }
@@ -192,9 +263,41 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
     scl[gg][threadIdx.x & 15] = (threadIdx.x & 8) ? ((p.shift && c < p.C) ? p.shift[c] : 0.0f)
                                                   : ((p.scale && c < p.C) ? p.scale[c] : 1.0f);
   }
+  if (RED && threadIdx.x < G * 32) {
+    // the producer's BN scale, shift, mean, invstd of the block's channels (LDS: not live across
+    // the FMAs)
+    const int gg = threadIdx.x >> 5, j = (threadIdx.x >> 3) & 3, k = threadIdx.x & 7, cc = c0 + 8 * gg + k;
+    const float* src = j == 0 ? p.rsc : (j == 1 ? p.rsh : (j == 2 ? p.rmi : p.rmi + p.C));
+    rpar[gg][j][k] = cc < p.C ? src[cc] : 0.0f;
+  }
   const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ty = lane / CGX, qx = lane - ty * CGX;   // ty >= TY: idle lane (60 of 64 used at TX 20 / 40)
   const int c = c0 + 8 * g, nv = min(8, p.C - c);
+  // DW_DGRAD_RED: this lane's RX chunks of the producer's z for tile t (prefetched a tile ahead)
+  // and its running (sum da, sum da * xhat) over the strip
+  const T* rzp = RED ? reinterpret_cast<const T*>(p.rz) + (long)n * p.H * p.W * p.rz_ld + p.rz_off : nullptr;
+  auto load_rz = [&](int t, Raw8<T> (&d)[DW_RX]) {
+    const int y = t * TY + ty;
+#pragma unroll
+    for (int i = 0; i < DW_RX; ++i) {
+      const int x = x0 + 4 * qx + i;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) d[i].v[k] = u32x4{0u, 0u, 0u, 0u};
+      if (ty < TY && y < p.H && x < p.W && nv > 0) load_raw8(rzp + ((long)y * p.W + x) * p.rz_ld + c, 8, d[i]);
+    }
+  };
+  float isc[8], ish[8];
+  if constexpr (BNIN) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      isc[k] = c + k < p.C ? p.isc[c + k] : 0.f;
+      ish[k] = c + k < p.C ? p.ish[c + k] : 0.f;
+    }
+  }
+  Raw8<T> rzc[RED ? DW_RX : 1], rzn[RED ? DW_RX : 1];
+  float ra1[8], ra2[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) { ra1[k] = 0.f; ra2[k] = 0.f; }
   // raw buffer resource over image n's rows (32-bit offsets: checked on the host)
   const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
                                                    (long)n * p.H * p.W * p.src_ld + p.src_off);
@@ -211,18 +314,26 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
       (void*)db, (short)0, (int)((long)p.H * p.W * p.dst_ld * (long)sizeof(T)), NT_RSRC3);
   const long srows = (long)p.N * p.tiles_y * p.tiles_x;
   const __amdgpu_buffer_rsrc_t rstat = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.stats, (short)0, MODE == DW_FWD_STATS ? (int)(srows * 2 * p.stats_ld * 4) : 0, NT_RSRC3);
+      (void*)p.stats, (short)0, STATS ? (int)(srows * 2 * p.stats_ld * 4) : 0, NT_RSRC3);
   const __amdgpu_buffer_rsrc_t rcnt = __builtin_amdgcn_make_buffer_rsrc(
-      (void*)p.stats_cnt, (short)0, MODE == DW_FWD_STATS ? (int)(srows * 4) : 0, NT_RSRC3);
+      (void*)p.stats_cnt, (short)0, STATS ? (int)(srows * 4) : 0, NT_RSRC3);
   // prologue: the first tile's TY + K - 1 rows
   for (int hy = 0; hy < TY + K - 1; ++hy)
     dw_row_dma<T, K, TX>(rs, myring + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
                          p.src_ld, lane);
+  if constexpr (RED) load_rz(t0, rzc);
   wait_vmcnt<0>();
   __syncthreads();
   for (int t = t0; t < t1; ++t) {
     const int y0 = t * TY;
     const bool more = t + 1 < t1;
+    if constexpr (BNIN) {
+      // the rows that landed for this tile (all TY + K - 1 of the strip's first tile)
+      if (t == t0) dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 - P, TY + K - 1, x0, p.H, p.W, nv > 0,
+                                                       isc, ish, p.iact, lane);
+      else dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 + P, TY, x0, p.H, p.W, nv > 0, isc, ish,
+                                               p.iact, lane);
+    }
     // the next tile's TY new rows y0 + TY + P .. y0 + 2 TY - 1 + P go to slots this tile does not read
     if (more) {
       int sl = (y0 + TY + 2 * P) % RB;
@@ -230,6 +341,7 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
         dw_row_dma<T, K, TX>(rs, myring + sl * ROWB, y0 + TY + P + hy, x0, c, p.H, p.W, p.C, p.src_ld, lane);
         sl = sl + 1 == RB ? 0 : sl + 1;
       }
+      if constexpr (RED) load_rz(t + 1, rzn);
     }
     const Raw8<T>* hp = ring + g * RB * RS + 4 * (ty < TY ? qx : 0);
     float acc[DW_RX][8];
@@ -271,7 +383,7 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
     // every wave issues exactly NST vector-memory instructions after its last DMA of this tile (the
     // stores below; statistics: two row stores and the count): the end-of-tile wait leaves them in
     // flight and waits for the next tile's rows only (vmcnt retires in issue order on gfx9)
-    constexpr int NST = DW_RX * (int)(sizeof(T) / 2) + (MODE == DW_FWD_STATS ? 3 : 0);
+    constexpr int NST = DW_RX * (int)(sizeof(T) / 2) + (STATS ? 3 : 0);
 #pragma unroll
     for (int i = 0; i < DW_RX; ++i) {
       const int x = x0 + 4 * qx + i;
@@ -298,8 +410,23 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
 #pragma unroll
       for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
         dw_bst16(rd, ok ? e * (uint32_t)sizeof(T) + 16u * h : NT_OOB, rv.v[h]);
+      if constexpr (RED) {
+        // the producer's BN + SiLU backward sums on dx as stored (bn_bwd_reduce_kernel's formula);
+        // out-of-image / idle lanes have z = 0 and dx = 0 chunks -- masked by ok
+        float gq[8], zv[8];
+        unpack8(rv, gq);
+        unpack8(rzc[i], zv);
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          const float a = zv[k] * rpar[g][0][k] + rpar[g][1][k];
+          const float da = p.ract == YMS_ACT_SILU ? gq[k] * dsilu_f(a) : gq[k];
+          const float xh = (zv[k] - rpar[g][2][k]) * rpar[g][3][k];
+          ra1[k] += ok ? da : 0.0f;
+          ra2[k] += ok ? da * xh : 0.0f;
+        }
+      }
     }
-    if (MODE == DW_FWD_STATS) {
+    if (STATS) {
       // one statistics row per spatial tile (conv_common.hpp contract; its pixel count goes to the
       // count table after the rows): sum and centred M2 over the tile's valid pixels, two passes
       // over the fp32 accumulators, wave butterflies in a fixed order
@@ -344,6 +471,32 @@ __global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v)) void dwconv_
     if (!p.waitall) wait_vmcnt<NST>();
     else wait_vmcnt<0>();   // dev A/B (YMS_DW_WAITALL=1): also drain the tile's stores
     __syncthreads();
+    if constexpr (RED) {
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < DW_RX; ++i) rzc[i] = rzn[i];
+      }
+    }
+  }
+  if constexpr (RED) {
+    // fixed-order butterfly over the wave's lanes; lanes 0..7 write channel c + lane of the strip's
+    // partial row blockIdx.x (every strip covers all channels through blockIdx.y)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) {
+        ra1[k] += __shfl_xor(ra1[k], m);
+        ra2[k] += __shfl_xor(ra2[k], m);
+      }
+    }
+    float a = 0.f, b = 0.f;
+#pragma unroll
+    for (int k = 0; k < 8; ++k)
+      if (k == lane) { a = ra1[k]; b = ra2[k]; }
+    if (lane < 8 && c + lane < p.C) {
+      p.rws[(long)blockIdx.x * 2 * p.C + c + lane] = a;
+      p.rws[(long)blockIdx.x * 2 * p.C + p.C + c + lane] = b;
+    }
   }
 }
 
@@ -362,7 +515,7 @@ struct DwWg {
 };
 constexpr int DW_WG_NT = 512, DW_WG_LPG = DW_WG_NT / DW_G;
 
-template <typename T, int K>
+template <typename T, int K, bool BNIN = false>
 __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
                                                                  float* ws) {
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1;
@@ -394,7 +547,7 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
     const int n = tile / per_img, rem = tile - n * per_img;
     const int y0 = (rem / p.tiles_x) * DW_TY, x0 = (rem % p.tiles_x) * DW_TX;
     __syncthreads();      // previous tile's LDS reads are done
-    dw_stage_halo<T, K, DW_WG_NT>(p, halo, n, y0, x0, c0);
+    dw_stage_halo<T, K, DW_WG_NT, BNIN>(p, halo, n, y0, x0, c0);
     for (int it = threadIdx.x; it < DZN; it += DW_WG_NT) {
       const int g2 = it / (DW_TY * DW_TX), r2 = it - g2 * (DW_TY * DW_TX);
       const int y = y0 + r2 / DW_TX, x = x0 + r2 % DW_TX, c = c0 + 8 * g2;
@@ -449,6 +602,144 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
       for (int rr = 0; rr < DW_TY * S; ++rr) s += red[((ddy * DW_TY * S + rr) * K + ddx) * 8 + k];
       const int cc = c0 + 8 * gg + k;
       if (cc < p.C) ws[((long)blockIdx.x * K * K + t) * p.C + cc] = s;
+    }
+  }
+}
+
+// wgrad, k = 3: the forward's strip walker (TY x TX tiles, RX = 4 pixels per lane, the input rows
+// in an LDS-DMA ring, the next tile's rows and dz chunks in flight while the current tile
+// computes).  Every lane keeps the 3 x 3 x 8 partial taps of its pixels in registers across the
+// whole strip: per kernel row it reads RX + 2 ring chunks and does 3 RX 8 FMAs against its RX dz
+// chunks.  At the end the 72 partials are summed over the wave's lanes by a fixed butterfly and
+// lane 0 writes ws[block][tap][c] (dwconv_wgrad_reduce_kernel sums the strips in a fixed order).
+// Replaces the 8 x 32-tile kernel above for k = 3, which staged each tile synchronously.
+template <typename T, int TX, int G, bool BNIN = false>
+__global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
+                                                                  float* ws) {
+  constexpr int K = 3, P = 1;
+  constexpr int CB = G * 8, TY = DwTy<TX>::v, CGX = TX / DW_RX;
+  constexpr int HW = TX + K - 1, RB = 2 * TY + K - 1, RS = dw_rs(HW);
+  constexpr int RING_B = G * RB * RS * (int)sizeof(Raw8<T>);
+  __shared__ __attribute__((aligned(16))) char smem[RING_B];
+  Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
+  const int per_img = p.tiles_x * p.ysplit;
+  const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
+  const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
+  const int x0 = tx * TX;
+  const int c0 = blockIdx.y * CB;
+  const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int ty = lane / CGX, qx = lane - ty * CGX;
+  const int c = c0 + 8 * g, nv = min(8, p.C - c);
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
+                                                   (long)n * p.H * p.W * p.src_ld + p.src_off);
+  const i32x4 rs = {(int)(uint32_t)ib, (int)(uint32_t)(ib >> 32) & 0xffff,
+                    (int)((long)p.H * p.W * p.src_ld * (long)sizeof(T)), NT_RSRC3};
+  const uint32_t myring = __builtin_amdgcn_readfirstlane(
+      (uint32_t)reinterpret_cast<uintptr_t>(ring + g * RB * RS));
+  constexpr uint32_t ROWB = RS * (uint32_t)sizeof(Raw8<T>);
+  const T* dzp = reinterpret_cast<const T*>(dz) + (long)n * p.H * p.W * dz_ld + dz_off;
+  // this lane's RX dz chunks of tile t (zeros outside the image / past C / idle lanes)
+  auto load_dz = [&](int t, Raw8<T> (&d)[DW_RX]) {
+    const int y = t * TY + ty;
+#pragma unroll
+    for (int i = 0; i < DW_RX; ++i) {
+      const int x = x0 + 4 * qx + i;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) d[i].v[k] = u32x4{0u, 0u, 0u, 0u};
+      if (ty < TY && y < p.H && x < p.W && nv > 0) load_raw8(dzp + ((long)y * p.W + x) * dz_ld + c, 8, d[i]);
+    }
+  };
+  float part[K][K][8];
+#pragma unroll
+  for (int a = 0; a < K; ++a)
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) part[a][b][k] = 0.0f;
+  float isc[8], ish[8];
+  if constexpr (BNIN) {
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      isc[k] = c + k < p.C ? p.isc[c + k] : 0.f;
+      ish[k] = c + k < p.C ? p.ish[c + k] : 0.f;
+    }
+  }
+  Raw8<T> dzc[DW_RX], dzn[DW_RX];
+  for (int hy = 0; hy < TY + K - 1; ++hy)
+    dw_row_dma<T, K, TX>(rs, myring + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
+                         p.src_ld, lane);
+  load_dz(t0, dzc);
+  wait_vmcnt<0>();
+  __syncthreads();
+  const Raw8<T>* hp = ring + g * RB * RS + 4 * (ty < TY ? qx : 0);
+  for (int t = t0; t < t1; ++t) {
+    const int y0 = t * TY;
+    const bool more = t + 1 < t1;
+    if constexpr (BNIN) {
+      if (t == t0) dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 - P, TY + K - 1, x0, p.H, p.W, nv > 0,
+                                                       isc, ish, p.iact, lane);
+      else dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 + P, TY, x0, p.H, p.W, nv > 0, isc, ish,
+                                               p.iact, lane);
+    }
+    if (more) {
+      int sl = (y0 + TY + 2 * P) % RB;
+      for (int hy = 0; hy < TY; ++hy) {
+        dw_row_dma<T, K, TX>(rs, myring + sl * ROWB, y0 + TY + P + hy, x0, c, p.H, p.W, p.C, p.src_ld, lane);
+        sl = sl + 1 == RB ? 0 : sl + 1;
+      }
+      load_dz(t + 1, dzn);
+    }
+    float d[DW_RX][8];
+#pragma unroll
+    for (int i = 0; i < DW_RX; ++i) unpack8(dzc[i], d[i]);
+    // idle lanes (ty >= TY) read row 0's slots: their dz is zero, but a slot of a later row may be
+    // unwritten LDS (NaN patterns) or landing now
+    int slot = (y0 + (ty < TY ? ty : 0)) % RB;
+#pragma unroll
+    for (int dy = 0; dy < K; ++dy) {
+      const Raw8<T>* row = hp + slot * RS;
+#pragma unroll
+      for (int q = 0; q < DW_RX + K - 1; ++q) {
+        float v[8];
+        unpack8(row[q], v);
+#pragma unroll
+        for (int i = 0; i < DW_RX; ++i) {
+          const int dx = q - i;
+          if (dx >= 0 && dx < K) {
+#pragma unroll
+            for (int k = 0; k < 8; ++k) part[dy][dx][k] += v[k] * d[i][k];
+          }
+        }
+      }
+      slot = slot + 1 == RB ? 0 : slot + 1;
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < DW_RX; ++i) dzc[i] = dzn[i];
+    }
+  }
+  // fixed-order butterfly over the wave's 64 lanes, lane 0 writes the block's 9 x 8 partial taps
+#pragma unroll
+  for (int a = 0; a < K; ++a)
+#pragma unroll
+    for (int b = 0; b < K; ++b)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        float v = part[a][b][k];
+#pragma unroll
+        for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+        part[a][b][k] = v;
+      }
+  if (lane == 0 && nv > 0) {
+#pragma unroll
+    for (int t = 0; t < K * K; ++t) {
+      float* o = ws + ((long)blockIdx.x * K * K + t) * p.C + c;
+      *reinterpret_cast<f32x4*>(o) = f32x4{part[t / K][t % K][0], part[t / K][t % K][1], part[t / K][t % K][2],
+                                           part[t / K][t % K][3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{part[t / K][t % K][4], part[t / K][t % K][5],
+                                               part[t / K][t % K][6], part[t / K][t % K][7]};
     }
   }
 }
@@ -572,6 +863,32 @@ static bool dw_image_fits(const yms_dw_shape* s, int ld) {
   return (long)s->h * s->w * ld * esz < (long)NT_OOB;
 }
 
+// k = 3 weight gradient on the strip walker (16-bit; YMS_DW_WG3=0 keeps the tile kernel: dev A/B)
+static bool dw_wg3(const yms_dw_shape* s) { return s->k == 3 && s->dtype != YMS_F32 && dw_env("YMS_DW_WG3", 1) != 0; }
+// its grid: the forward's tiles and channel blocks; strips as long as whole rounds of the resident
+// blocks allow (cost model as dw_strip_grid, plus the per-strip butterfly and partial row ~ 3 tiles)
+// channel groups per wgrad block: 4 by default (two 256-thread blocks per CU at ~230 VGPRs);
+// YMS_DW_WG3_G=8 uses the forward's 64-channel blocks where they apply (dev A/B)
+static int dw_wg3_g(const yms_dw_shape* s) { return dw_env("YMS_DW_WG3_G", 4) == 8 ? dw_fwd_g(s) : 4; }
+static dim3 dw_wg3_grid(const yms_dw_shape* s, DwParams& p) {
+  dw_fwd_tiles(s, p.tiles_x, p.tiles_y);
+  const int TY = dw_fwd_ty(dw_fwd_tx(s)), G = dw_wg3_g(s);
+  const long cg = (s->c + 8 * G - 1) / (8 * G);
+  const long base = (long)s->n * p.tiles_x * cg;
+  const long slots = (G == 8 ? 1l : 2l) * conv_cu_count();
+  double best = 1e30;
+  int best_tps = p.tiles_y;
+  for (int tps = p.tiles_y; tps >= 1; --tps) {
+    const long ys = (p.tiles_y + tps - 1) / tps;
+    const long rounds = (base * ys + slots - 1) / slots;
+    const double cost = (double)rounds * (tps * TY + s->k - 1 + 3 * TY);
+    if (cost < best * 0.999) { best = cost; best_tps = tps; }
+  }
+  p.tps = best_tps;
+  p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
+  return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
+}
+
 // spatial partitions of the wgrad grid: about 1024 blocks in total over the channel groups (two
 // 512-thread blocks fit a CU), each walking several tiles so the ws rows stay few
 static int dw_wgrad_blocks(const yms_dw_shape* s) {
@@ -659,11 +976,13 @@ int yms_dwconv_stats_rows(const yms_dw_shape* s) {
   return dw_fwd_tiles(s, tx, ty);
 }
 
-yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
-                          int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
-                          int stats_ld, void* stream) {
+static yms_status dw_fwd_impl(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
+                              int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
+                              int stats_ld, const float* isc, const float* ish, int iact, void* stream) {
   if (!dw_shape_ok(s) || !x || !w || !y || !dw_view_ok(x_ld, x_off, s->c) || !dw_view_ok(y_ld, y_off, s->c))
     return YMS_ERR_INVALID;
+  const bool bnin = isc != nullptr;
+  if (bnin && (!ish || !stats || s->dtype == YMS_F32)) return YMS_ERR_INVALID;
   if (stats && stats_ld < s->c) return YMS_ERR_INVALID;
   if (!dw_image_fits(s, x_ld) || !dw_image_fits(s, y_ld)) return YMS_ERR_UNSUPPORTED;
   if (stats && (long)yms_dwconv_stats_rows(s) * 2 * stats_ld * 4 >= (long)NT_OOB) return YMS_ERR_UNSUPPORTED;
@@ -673,9 +992,20 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   p.scale = scale; p.shift = shift; p.act = act; p.stats = stats; p.stats_ld = stats_ld;
   if (stats) p.stats_cnt = stats + (long)yms_dwconv_stats_rows(s) * 2 * stats_ld;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
+  p.isc = isc; p.ish = ish; p.iact = iact;
   const dim3 grid = dw_strip_grid(s, p);
   hipStream_t st = (hipStream_t)stream;
   const int TX = dw_fwd_tx(s);
+  if (bnin) {
+    if (dw_fwd_g(s) == 8) {
+      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_STATS_BNIN, TXX, 8>), grid,
+                                                             dim3(512), 0, st, p)));
+      return launch_status();
+    }
+    YMS_DW_T16(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_STATS_BNIN, TXX>),
+                                                                         grid, dim3(256), 0, st, p))));
+    return launch_status();
+  }
   if (dw_fwd_g(s) == 8) {
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
       if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_STATS, TXX, 8>), grid, dim3(512), 0, st, p);
@@ -688,6 +1018,21 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
     else hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_AFFINE, TXX>), grid, dim3(256), 0, st, p);
   })));
   return launch_status();
+}
+
+yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
+                          int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
+                          int stats_ld, void* stream) {
+  return dw_fwd_impl(s, x, x_ld, x_off, w, y, y_ld, y_off, scale, shift, act, stats, stats_ld, nullptr, nullptr, 0,
+                     stream);
+}
+
+yms_status yms_dwconv_fwd_bnin(const yms_dw_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
+                               const float* in_shift, int in_act, const float* w, void* y, int y_ld, int y_off,
+                               float* stats, int stats_ld, void* stream) {
+  if (!in_scale) return YMS_ERR_INVALID;
+  return dw_fwd_impl(s, z, z_ld, z_off, w, y, y_ld, y_off, nullptr, nullptr, 0, stats, stats_ld, in_scale, in_shift,
+                     in_act, stream);
 }
 
 yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w, void* dx,
@@ -712,31 +1057,111 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
   return launch_status();
 }
 
+int yms_dwconv_dgrad_rows(const yms_dw_shape* s) {
+  if (!dw_shape_ok(s)) return 0;
+  DwParams p{};
+  return (int)dw_strip_grid(s, p).x;
+}
+
+yms_status yms_dwconv_dgrad_bnred(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w,
+                                  void* dx, int dx_ld, int dx_off, const void* rz, int rz_ld, int rz_off,
+                                  const float* rscale, const float* rshift, const float* rmean_invstd, int ract,
+                                  float* rws, void* stream) {
+  if (!dw_shape_ok(s) || !dz || !w || !dx || !rz || !rscale || !rshift || !rmean_invstd || !rws ||
+      !dw_view_ok(dz_ld, dz_off, s->c) || !dw_view_ok(dx_ld, dx_off, s->c) || !dw_view_ok(rz_ld, rz_off, s->c))
+    return YMS_ERR_INVALID;
+  if (!dw_image_fits(s, dz_ld) || !dw_image_fits(s, dx_ld)) return YMS_ERR_UNSUPPORTED;
+  DwParams p{};
+  p.src = (const char*)dz; p.src_ld = dz_ld; p.src_off = dz_off; p.w = w;
+  p.dst = (char*)dx; p.dst_ld = dx_ld; p.dst_off = dx_off; p.accumulate = 0;
+  p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
+  p.rz = (const char*)rz; p.rz_ld = rz_ld; p.rz_off = rz_off;
+  p.rsc = rscale; p.rsh = rshift; p.rmi = rmean_invstd; p.ract = ract; p.rws = rws;
+  const dim3 grid = dw_strip_grid(s, p);
+  hipStream_t st = (hipStream_t)stream;
+  const int TX = dw_fwd_tx(s);
+  if (dw_fwd_g(s) == 8) {
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_DGRAD_RED, TXX, 8>), grid,
+                                                           dim3(512), 0, st, p)));
+    return launch_status();
+  }
+  YMS_DW_T(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_DGRAD_RED, TXX>),
+                                                                     grid, dim3(256), 0, st, p))));
+  return launch_status();
+}
+
 size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s) {
   if (!dw_shape_ok(s)) return 0;
+  if (dw_wg3(s)) {
+    DwParams p{};
+    return (size_t)dw_wg3_grid(s, p).x * s->k * s->k * s->c * sizeof(float);
+  }
   return (size_t)dw_wgrad_blocks(s) * s->k * s->k * s->c * sizeof(float);
 }
 
-yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
-                            int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream) {
+static yms_status dw_wgrad_impl(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
+                                int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, const float* isc,
+                                const float* ish, int iact, void* stream) {
   if (!dw_shape_ok(s) || !x || !dz || !ws || !dw || !dw_view_ok(x_ld, x_off, s->c) || !dw_view_ok(dz_ld, dz_off, s->c))
     return YMS_ERR_INVALID;
   if (ws_bytes < yms_dwconv_wgrad_ws_bytes(s)) return YMS_ERR_INVALID;
+  const bool bnin = isc != nullptr;
+  if (bnin && (!ish || s->dtype == YMS_F32)) return YMS_ERR_INVALID;
   DwParams p{};
   p.src = (const char*)x; p.src_ld = x_ld; p.src_off = x_off;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
+  p.isc = isc; p.ish = ish; p.iact = iact;
+  if (dw_wg3(s)) {
+    if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
+    const dim3 grid = dw_wg3_grid(s, p);
+    hipStream_t st = (hipStream_t)stream;
+    const int TX = dw_fwd_tx(s);
+    if (bnin) {
+      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 4, true>), grid,
+                                                             dim3(256), 0, st, p, (const char*)dz, dz_ld, dz_off, ws)));
+    } else if (dw_wg3_g(s) == 8) {
+      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 8>), grid, dim3(512), 0,
+                                                             st, p, (const char*)dz, dz_ld, dz_off, ws)));
+    } else {
+      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 4>), grid, dim3(256), 0,
+                                                             st, p, (const char*)dz, dz_ld, dz_off, ws)));
+    }
+    yms_status e = launch_status();
+    if (e != YMS_OK) return e;
+    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * 9 + 63) / 64)), dim3(1024), 0, st, ws,
+                       (int)grid.x, s->c, 9, dw, accumulate);
+    return launch_status();
+  }
   dw_tiles(s, p.tiles_x, p.tiles_y);
   const int blocks = dw_wgrad_blocks(s);
   dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
   hipStream_t st = (hipStream_t)stream;
-  YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK>), grid, dim3(DW_WG_NT), 0, st, p,
-                                                      (const char*)dz, dz_ld, dz_off, ws)));
+  if (bnin) {
+    YMS_DW_T16(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK, true>), grid, dim3(DW_WG_NT), 0,
+                                                          st, p, (const char*)dz, dz_ld, dz_off, ws)));
+  } else {
+    YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK>), grid, dim3(DW_WG_NT), 0, st, p,
+                                                        (const char*)dz, dz_ld, dz_off, ws)));
+  }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
   const int KK2 = s->k * s->k;
   hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
                      blocks, s->c, KK2, dw, accumulate);
   return launch_status();
+}
+
+yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
+                            int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream) {
+  return dw_wgrad_impl(s, x, x_ld, x_off, dz, dz_ld, dz_off, ws, ws_bytes, dw, accumulate, nullptr, nullptr, 0, stream);
+}
+
+yms_status yms_dwconv_wgrad_bnin(const yms_dw_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
+                                 const float* in_shift, int in_act, const void* dz, int dz_ld, int dz_off, float* ws,
+                                 size_t ws_bytes, float* dw, int accumulate, void* stream) {
+  if (!in_scale) return YMS_ERR_INVALID;
+  return dw_wgrad_impl(s, z, z_ld, z_off, dz, dz_ld, dz_off, ws, ws_bytes, dw, accumulate, in_scale, in_shift, in_act,
+                       stream);
 }
 
 yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,

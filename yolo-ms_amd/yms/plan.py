@@ -205,6 +205,8 @@ class ConvOp:
         self.pb = b.param(mod.bn, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
+        self.red_rows = 0        # > 0: its BN-backward partial rows come from its consumer's dgrad
+        self.bnin_by = None      # depthwise consumer that forms act(BN(z)) itself (no affine pass)
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -287,8 +289,9 @@ class ConvOp:
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
-        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
-               base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
+        if self.bnin_by is None:
+            L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+                   base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
 
     def plan_grads(self, T):
         T.read(self.y)
@@ -302,7 +305,11 @@ class ConvOp:
         ws = rt.gbase + rt.plan.gscratch["bwd"]
         coef = rt.gbase + rt.plan.gscratch["coef"]
         z = base + self.z
-        if BN_FUSED_FINALIZE:
+        if self.red_rows:
+            # the partial rows were written by the consuming depthwise dgrad (DWConvOp.bnred)
+            L.call("yms_bn_act_bwd_finalize", c, ws, self.red_rows, self.npix,
+                   rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        elif BN_FUSED_FINALIZE:
             # one launch: partial sums + (last block) dgamma / dbeta / the two apply coefficients
             L.call("yms_bn_act_bwd_reduce_finalize", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
                    base + self.sh, base + self.mi, self.act, ws, rt.cnt(self.cnt), rt.pgrad(self.pg),
@@ -329,16 +336,20 @@ class ConvOp:
             return
         gres = rt.g(r) if r is not None else None
         gro = (r.buf.ld, r.off) if r is not None else (0, 0)
+        # dz overwrites z in place -- unless the depthwise consumer forms act(BN(z)) itself: its
+        # weight gradient (side stream) may still be reading z, so dz goes to the activation
+        # buffer it never materialised (same layout: fresh buffer, ld = r8(c), offset 0)
+        dz = rt.a(y) if self.bnin_by is not None else z
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
-               base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, gres, gro[0], gro[1], self.acc_res,
+               base + self.sh, base + self.mi, coef, self.act, dz, self.zld, 0, gres, gro[0], gro[1], self.acc_res,
                rt.st)
         if x.buf.needs_grad:
-            L.call("yms_conv_dgrad", self.sp, z, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+            L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
                    self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             wsz = self.wg_ws
-            L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
+            L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, 0,
                    rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
 
     def grad_params(self):
@@ -361,6 +372,8 @@ class BiasConvOp:
         self.pbias = b.param(conv, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
+        self.red_rows = 0        # > 0: its BN-backward partial rows come from its consumer's dgrad
+        self.bnin_by = None      # depthwise consumer that forms act(BN(z)) itself (no affine pass)
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -440,6 +453,8 @@ class DWConvOp(ConvOp):
         self.pb = b.param(mod.bn, "bias")
         self.flops = 0          # not an MFMA contraction: excluded from the conv roofline
         self.dw_flops = 2 * self.npix * c * k * k
+        self.bnred = None       # producer ConvOp whose BN-backward reduce is fused into this dgrad
+        self.bnin = None        # producer ConvOp whose act(BN(z)) this op forms from z (fwd, wgrad)
 
     def layout(self, plan, La, Le):
         es, c = plan.es, self.c
@@ -458,6 +473,9 @@ class DWConvOp(ConvOp):
             plan.need_scratch("coef", 8 * c)
             plan.need_scratch("wgrad", L.lib().yms_dwconv_wgrad_ws_bytes(self.sp))
             self.cnt = plan.counter()
+            if self.bnred is not None:
+                self.bnred.red_rows = L.lib().yms_dwconv_dgrad_rows(self.sp)
+                plan.need_scratch("bwd", 4 * 2 * c * self.bnred.red_rows)
 
     def pack_specs(self):
         return []
@@ -478,8 +496,13 @@ class DWConvOp(ConvOp):
             return
         base = rt.base
         stats = base + rt.plan.scratch["stats"]
-        L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, base + self.z, self.zld, 0, None, None,
-               L.ACT_NONE, stats, self.stats_ld, rt.st)
+        if self.bnin is not None:
+            p = self.bnin
+            L.call("yms_dwconv_fwd_bnin", self.sp, base + p.z, p.zld, 0, base + p.sc, base + p.sh, p.act, w,
+                   base + self.z, self.zld, 0, stats, self.stats_ld, rt.st)
+        else:
+            L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, base + self.z, self.zld, 0, None, None,
+                   L.ACT_NONE, stats, self.stats_ld, rt.st)
         bn = self.mod.bn
         L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
@@ -501,13 +524,24 @@ class DWConvOp(ConvOp):
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, rt.g(y), y.buf.ld, y.off, base + self.sc,
                base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, None, 0, 0, 0, rt.st)
         w = self.mod.conv.weight.data_ptr()
-        if x.buf.needs_grad:
+        if x.buf.needs_grad and self.bnred is not None:
+            # dx is the producer's whole activation gradient: its BN-backward partial sums come out
+            # of the same pass (the producer's finalize reads them from the "bwd" scratch next)
+            p = self.bnred
+            L.call("yms_dwconv_dgrad_bnred", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off,
+                   base + p.z, p.zld, 0, base + p.sc, base + p.sh, base + p.mi, p.act, ws, rt.st)
+        elif x.buf.needs_grad:
             L.call("yms_dwconv_dgrad", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             wsz = L.lib().yms_dwconv_wgrad_ws_bytes(self.sp)
-            L.call("yms_dwconv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
-                   rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
+            if self.bnin is not None:
+                p = self.bnin
+                L.call("yms_dwconv_wgrad_bnin", self.sp, base + p.z, p.zld, 0, base + p.sc, base + p.sh, p.act, z,
+                       self.zld, 0, rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
+            else:
+                L.call("yms_dwconv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
+                       rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
 
 
 class AddOp:
@@ -684,6 +718,7 @@ class Plan:
         self.scratch_req = {}
         self.n_counters = 0
         self.stem_inputs = self._find_stems()
+        self._find_dw_bnred()
         La, Le = Layout(), Layout()
         for buf in self.bufs:
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
@@ -707,6 +742,11 @@ class Plan:
             self.seed_acc = [T.write(v) for v in self.outputs]
             for op in reversed(self.ops):
                 op.plan_grads(T)
+            for op in self.ops:
+                if getattr(op, "bnred", None) is not None and op.acc_x:
+                    # the fused dgrad stores: keep the separate reduce if dx must accumulate
+                    op.bnred.red_rows = 0
+                    op.bnred = None
             self.gzero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.idx in T.zero]
             self.gzero_ranges.append((self.gscratch["cnt"], 16 * max(self.n_counters, 1)))
         self.flops = sum(op.flops for op in self.ops)
@@ -742,6 +782,42 @@ class Plan:
                 op.stem_input = i
                 out[i] = op
         return out
+
+    def _find_dw_bnred(self):
+        """Depthwise convs whose input is the whole output of the Conv op right before them and is
+        read by nothing else (the MS-Block IB: 1x1 expand -> BN -> SiLU -> depthwise): the
+        depthwise dgrad writes that activation gradient in full, so it also produces the expand
+        conv's BN-backward partial sums (yms_dwconv_dgrad_bnred) and the expand conv skips its
+        reduce pass; and (BNIN) the depthwise forward and weight gradient form act(BN(z)) of the
+        expand conv from its z while staging, so the expand conv's affine_act pass goes.  Both are
+        opt-in (YMS_DW_BNRED=1, YMS_DW_BNIN=1), measured slower on YOLO-MS-S (interleaved, one box):
+        BNRED 37.06 -> 37.6 ms (the fused dgrad runs at half occupancy; the reduce it replaces
+        re-read data still in the MALL), BNIN 38.24 -> 38.72 ms (affine -0.87 ms, but the
+        converting forward +0.33 ms, the out-of-place dz apply +0.8 ms and the converting weight
+        gradient +2.1 ms on the side stream).  16-bit training only."""
+        bnred = os.environ.get("YMS_DW_BNRED", "0") == "1"
+        bnin = os.environ.get("YMS_DW_BNIN", "0") == "1"
+        if not self.training or self.dt == L.F32 or not (bnred or bnin):
+            return
+        for i, d in enumerate(self.ops):
+            if type(d) is not DWConvOp or i == 0:
+                continue
+            p, x = self.ops[i - 1], d.x
+            if type(p) is not ConvOp or p.stem_input is not None or p.y.buf is not x.buf:
+                continue
+            if p.y.off != x.off or p.y.c != x.c or x.off != 0 or x.buf.zero or not x.buf.needs_grad:
+                continue
+            if any(x.buf is o.buf for o in self.outputs):
+                continue
+            readers = [op for op in self.ops if op is not p
+                       and any(isinstance(a, View) and a.buf is x.buf for a in vars(op).values())]
+            if readers != [d] or p.res is not None or x.buf.ld != r8(p.c):
+                continue
+            if bnred:
+                d.bnred = p
+            if bnin:
+                d.bnin = p
+                p.bnin_by = d
 
     def counter(self):
         """Reserve one 16-B arrival counter in the grad scratch (-> its index)."""
