@@ -37,6 +37,7 @@ def test_dwconv_fwd_dgrad_wgrad(shp, dt, tx, monkeypatch):
     monkeypatch.setenv("YMS_DW_G", "4" if tx.endswith("g4") else "0")
     # k = 3 weight gradient: strip walker (4 or 8 channel groups) or the tile kernel ("w" variant)
     monkeypatch.setenv("YMS_DW_WG3", "0" if tx.endswith("w") else "1")
+    monkeypatch.setenv("YMS_DW_WGK", "0" if tx.endswith("w") else "1")   # k >= 5: opt-in rows-over-waves kernel
     monkeypatch.setenv("YMS_DW_WG3_G", "8" if tx == "0" else "4")
     n, h, w, c, k = shp
     dtype = DT[dt]

@@ -744,6 +744,112 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
   }
 }
 
+// wgrad, k = 5 / 7 / 9: the strip walker with the kernel rows spread over the waves -- a block of K
+// waves owns 8 channels, wave dy accumulates the K x 8 partial taps of kernel row dy for the
+// RX = 4 pixels of each lane (K x 8 registers instead of K x K x 8).  The input rows (8 channels)
+// sit in one LDS-DMA ring shared by the K waves (row hy loaded by wave hy % K), the next tile's
+// rows and the lanes' dz chunks in flight while the current tile computes; fixed-order butterfly
+// per wave, ws[strip][dy K + dx][c] partial rows, dwconv_wgrad_reduce_kernel sums the strips.
+// (Opt-in, see dw_wgk: the 8 x 32-tile kernel stays the default for k >= 5.)
+template <int K> struct DwWgkOcc { static constexpr int v = K == 5 ? 3 : (K == 7 ? 2 : 1); };
+template <typename T, int K, int TX>
+__global__ __launch_bounds__(K * 64, DwWgkOcc<K>::v) void dwconv_wgradk_kernel(DwParams p, const char* dz, int dz_ld,
+                                                                              int dz_off, float* ws) {
+  constexpr int P = K / 2, TY = DwTy<TX>::v, CGX = TX / DW_RX;
+  constexpr int HW = TX + K - 1, RB = 2 * TY + K - 1, RS = dw_rs(HW);
+  __shared__ __attribute__((aligned(16))) char smem[RB * RS * (int)sizeof(Raw8<T>)];
+  Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
+  const int per_img = p.tiles_x * p.ysplit;
+  const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
+  const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
+  const int x0 = tx * TX;
+  const int c = blockIdx.y * 8, nv = min(8, p.C - c);
+  const int dy = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(dy);
+  const int ty = lane / CGX, qx = lane - ty * CGX;
+  const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
+                                                   (long)n * p.H * p.W * p.src_ld + p.src_off);
+  const i32x4 rs = {(int)(uint32_t)ib, (int)(uint32_t)(ib >> 32) & 0xffff,
+                    (int)((long)p.H * p.W * p.src_ld * (long)sizeof(T)), NT_RSRC3};
+  const uint32_t ring0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(ring));
+  constexpr uint32_t ROWB = RS * (uint32_t)sizeof(Raw8<T>);
+  const T* dzp = reinterpret_cast<const T*>(dz) + (long)n * p.H * p.W * dz_ld + dz_off;
+  auto load_dz = [&](int t, Raw8<T> (&d)[DW_RX]) {
+    const int y = t * TY + ty;
+#pragma unroll
+    for (int i = 0; i < DW_RX; ++i) {
+      const int x = x0 + 4 * qx + i;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) d[i].v[k] = u32x4{0u, 0u, 0u, 0u};
+      if (ty < TY && y < p.H && x < p.W && nv > 0) load_raw8(dzp + ((long)y * p.W + x) * dz_ld + c, 8, d[i]);
+    }
+  };
+  float part[K][8];
+#pragma unroll
+  for (int b = 0; b < K; ++b)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[b][k] = 0.0f;
+  Raw8<T> dzc[DW_RX], dzn[DW_RX];
+  for (int hy = wv; hy < TY + K - 1; hy += K)
+    dw_row_dma<T, K, TX>(rs, ring0 + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
+                         p.src_ld, lane);
+  load_dz(t0, dzc);
+  wait_vmcnt<0>();
+  __syncthreads();
+  const Raw8<T>* hp = ring + 4 * (ty < TY ? qx : 0);
+  for (int t = t0; t < t1; ++t) {
+    const int y0 = t * TY;
+    const bool more = t + 1 < t1;
+    if (more) {
+      for (int hy = wv; hy < TY; hy += K)
+        dw_row_dma<T, K, TX>(rs, ring0 + ((y0 + TY + 2 * P + hy) % RB) * ROWB, y0 + TY + P + hy, x0, c, p.H, p.W,
+                             p.C, p.src_ld, lane);
+      load_dz(t + 1, dzn);
+    }
+    float d[DW_RX][8];
+#pragma unroll
+    for (int i = 0; i < DW_RX; ++i) unpack8(dzc[i], d[i]);
+    // input row y0 + ty + dy - P (idle lanes: row 0's, their dz is zero)
+    const Raw8<T>* row = hp + ((y0 + (ty < TY ? ty : 0) + dy) % RB) * RS;
+#pragma unroll
+    for (int q = 0; q < DW_RX + K - 1; ++q) {
+      float v[8];
+      unpack8(row[q], v);
+#pragma unroll
+      for (int i = 0; i < DW_RX; ++i) {
+        const int dx = q - i;
+        if (dx >= 0 && dx < K) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) part[dx][k] += v[k] * d[i][k];
+        }
+      }
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < DW_RX; ++i) dzc[i] = dzn[i];
+    }
+  }
+#pragma unroll
+  for (int b = 0; b < K; ++b)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) {
+      float v = part[b][k];
+#pragma unroll
+      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
+      part[b][k] = v;
+    }
+  if (lane == 0 && nv > 0) {
+#pragma unroll
+    for (int b = 0; b < K; ++b) {
+      float* o = ws + ((long)blockIdx.x * K * K + dy * K + b) * p.C + c;
+      *reinterpret_cast<f32x4*>(o) = f32x4{part[b][0], part[b][1], part[b][2], part[b][3]};
+      *reinterpret_cast<f32x4*>(o + 4) = f32x4{part[b][4], part[b][5], part[b][6], part[b][7]};
+    }
+  }
+}
+
 // dw[c][t] (+)= sum_b ws[b][t][c]: 64 outputs per block, 16 waves; wave w sums blocks
 // b = w (mod 16) into 4 independent partials (4 loads in flight per lane; one dependent chain
 // over ~500 rows made the reduce latency-bound), then a fixed-order tree over the waves
@@ -882,6 +988,30 @@ static dim3 dw_wg3_grid(const yms_dw_shape* s, DwParams& p) {
     const long ys = (p.tiles_y + tps - 1) / tps;
     const long rounds = (base * ys + slots - 1) / slots;
     const double cost = (double)rounds * (tps * TY + s->k - 1 + 3 * TY);
+    if (cost < best * 0.999) { best = cost; best_tps = tps; }
+  }
+  p.tps = best_tps;
+  p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
+  return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
+}
+
+// k = 5 / 7 / 9 weight gradient with the kernel rows over the waves: opt-in (YMS_DW_WGK=1), measured
+// no better than the tile kernel at B = 64 (k5@80 c128 184 -> 202 us, k7@40 c256 149 -> 138 us,
+// k9@20 c512 138 -> 320 us: 8-channel blocks read 16 B per pixel line, and k = 9 spills at one
+// 9-wave block per CU; profiles/r03n_dw_wgradk_micro.txt).  Its grid: strips x 8-channel groups.
+static bool dw_wgk(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32 && dw_env("YMS_DW_WGK", 0) == 1; }
+static dim3 dw_wgk_grid(const yms_dw_shape* s, DwParams& p) {
+  dw_fwd_tiles(s, p.tiles_x, p.tiles_y);
+  const int TY = dw_fwd_ty(dw_fwd_tx(s));
+  const long cg = (s->c + 7) / 8;
+  const long base = (long)s->n * p.tiles_x * cg;
+  const long slots = (long)(s->k == 5 ? 3 : (s->k == 7 ? 2 : 1)) * conv_cu_count();
+  double best = 1e30;
+  int best_tps = p.tiles_y;
+  for (int tps = p.tiles_y; tps >= 1; --tps) {
+    const long ys = (p.tiles_y + tps - 1) / tps;
+    const long rounds = (base * ys + slots - 1) / slots;
+    const double cost = (double)rounds * (tps * TY + s->k - 1 + 2 * TY);
     if (cost < best * 0.999) { best = cost; best_tps = tps; }
   }
   p.tps = best_tps;
@@ -1096,7 +1226,13 @@ size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s) {
     DwParams p{};
     return (size_t)dw_wg3_grid(s, p).x * s->k * s->k * s->c * sizeof(float);
   }
-  return (size_t)dw_wgrad_blocks(s) * s->k * s->k * s->c * sizeof(float);
+  const size_t tile = (size_t)dw_wgrad_blocks(s) * s->k * s->k * s->c * sizeof(float);
+  if (dw_wgk(s)) {
+    // the input-affine (BNIN) weight gradient keeps the tile kernel: size for both
+    DwParams p{};
+    return std::max(tile, (size_t)dw_wgk_grid(s, p).x * s->k * s->k * s->c * sizeof(float));
+  }
+  return tile;
 }
 
 static yms_status dw_wgrad_impl(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
@@ -1130,6 +1266,26 @@ static yms_status dw_wgrad_impl(const yms_dw_shape* s, const void* x, int x_ld, 
     if (e != YMS_OK) return e;
     hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * 9 + 63) / 64)), dim3(1024), 0, st, ws,
                        (int)grid.x, s->c, 9, dw, accumulate);
+    return launch_status();
+  }
+  if (dw_wgk(s) && !bnin) {
+    if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
+    const dim3 grid = dw_wgk_grid(s, p);
+    hipStream_t st = (hipStream_t)stream;
+    const int TX = dw_fwd_tx(s);
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
+      if (s->k == 5) hipLaunchKernelGGL((dwconv_wgradk_kernel<TT, 5, TXX>), grid, dim3(5 * 64), 0, st, p,
+                                        (const char*)dz, dz_ld, dz_off, ws);
+      else if (s->k == 7) hipLaunchKernelGGL((dwconv_wgradk_kernel<TT, 7, TXX>), grid, dim3(7 * 64), 0, st, p,
+                                             (const char*)dz, dz_ld, dz_off, ws);
+      else hipLaunchKernelGGL((dwconv_wgradk_kernel<TT, 9, TXX>), grid, dim3(9 * 64), 0, st, p, (const char*)dz,
+                              dz_ld, dz_off, ws);
+    }));
+    yms_status e = launch_status();
+    if (e != YMS_OK) return e;
+    const int KK2 = s->k * s->k;
+    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
+                       (int)grid.x, s->c, KK2, dw, accumulate);
     return launch_status();
   }
   dw_tiles(s, p.tiles_x, p.tiles_y);
