@@ -36,7 +36,10 @@ def family(name):
         nums = [a.strip() for a in m.group(1).split(",") if a.strip().isdigit()]
         epi = int(nums[1])
         return "conv_fwd" if epi <= 1 else "conv_dgrad"
-    if "conv_wgrad_kernel" in name or "wgrad_reduce_kernel" in name:
+    # every weight-gradient kernel behind yms_conv_wgrad: the im2col TT kernel, the LDS-DMA ring
+    # (wgrad_ring.hip), the halo-tiled 3x3 kernel (wgrad_halo.hip) and their split-K reducer
+    if ("conv_wgrad_kernel" in name or "conv_wgrad_ring_kernel" in name or "conv_wgrad_halo_kernel" in name
+            or "wgrad_reduce_kernel" in name) and "stem" not in name and "dwconv" not in name:
         return "conv_wgrad"
     m = re.search(r"yms::(\w+?)(?:_kernel)?[(<]", name) or re.search(r"_ZN3yms\d+(\w+?)(?:_kernel)?I", name) \
         or re.search(r"N3yms\d+(\w+)E", name)
@@ -47,7 +50,8 @@ def family(name):
 
 def is_call_head(name):
     """Kernels that start one yms_conv_* call (the wgrad reducer does not)."""
-    return "conv_nt_kernel" in name or "conv_ntp_kernel" in name or "conv_wgrad_kernel" in name
+    return ("conv_nt_kernel" in name or "conv_ntp_kernel" in name or "conv_wgrad_kernel" in name
+            or "conv_wgrad_ring_kernel" in name or "conv_wgrad_halo_kernel" in name)
 
 
 def stats(path):
