@@ -63,3 +63,12 @@ print("totals (ms):", {n: (c, round(t, 3)) for n, (c, t) in sorted(tot.items(), 
 print("top calls:")
 for n, k, t, fl in sorted(rows, key=lambda r: -r[2])[:40]:
     print(f"{n:28s} {k:34s} {t * 1e3:8.1f} us {fl / (t * 1e-3) / 1e12 if fl else 0:7.1f} TF/s")
+agg = {}
+for n, k, t, fl in rows:
+    a = agg.setdefault((n, k), [0, 0.0, 0.0])
+    a[0] += 1
+    a[1] += t
+    a[2] += fl
+print("per layer shape (count, total us, TF/s):")
+for (n, k), (c, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:45]:
+    print(f"{n:28s} {k:34s} x{c:2d} {t * 1e3:9.1f} us {fl / (t * 1e-3) / 1e12 if fl else 0:7.1f} TF/s")

@@ -424,6 +424,50 @@ __global__ __launch_bounds__(32 * TY) void bn_bwd_finalize_kernel(int c, const f
   }
 }
 
+// latency-shaped variant (dev A/B, YMS_BN_FIN_V2=1): 8 channels x 32 row lanes, each lane issues
+// ALL its rows' loads before the first add -- one L2 round trip instead of a dependent chain of 16.
+// Measured slower in the step, interleaved on one box (round 3, profiles/r03q_bn_finalize_ab.txt):
+// YOLOv8-s 19.15-19.20 -> 19.32-19.36 ms, YOLO-MS-S 38.26 -> 38.56 ms.  Its 4x more blocks wait
+// for CU slots the side stream's weight-gradient blocks hold: inside the step the finalize's time
+// is slot waiting, not load latency (the same outcome as round 2's float4 variant).
+constexpr int FIN2_RL = 32, FIN2_MAXR = 16;
+__global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(int c, const float* ws, int rows, long count,
+                                                               float* dgamma, float* dbeta, float* coef) {
+  __shared__ double red[2][FIN2_RL][9];
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int ch = blockIdx.x * 8 + tx;
+  double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
+  if (ch < c) {
+    for (int r0 = ty; r0 < rows; r0 += FIN2_RL * FIN2_MAXR) {
+      float v1[FIN2_MAXR], v2[FIN2_MAXR];
+#pragma unroll
+      for (int u = 0; u < FIN2_MAXR; ++u) {
+        const int r = r0 + FIN2_RL * u;
+        v1[u] = r < rows ? ws[(long)r * 2 * c + ch] : 0.f;
+        v2[u] = r < rows ? ws[(long)r * 2 * c + c + ch] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < FIN2_MAXR; ++u) {
+        a1[u & 3] += (double)v1[u];
+        a2[u & 3] += (double)v2[u];
+      }
+    }
+  }
+  red[0][ty][tx] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
+  red[1][ty][tx] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
+  __syncthreads();
+  if (ty == 0 && ch < c) {
+    double t1 = 0.0, t2 = 0.0;
+    for (int k = 0; k < FIN2_RL; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
+    if (dbeta) dbeta[ch] = (float)t1;
+    if (dgamma) dgamma[ch] = (float)t2;
+    if (coef) {
+      coef[ch] = (float)(t1 / (double)count);
+      coef[c + ch] = (float)(t2 / (double)count);
+    }
+  }
+}
+
 template <typename T>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, const T* z, int z_ld, int z_off,
                                                            const T* gy, int gy_ld, int gy_off, const float* scale,
@@ -856,7 +900,11 @@ yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count,
   static const int wide = getenv("YMS_BN_FIN_1024") ? atoi(getenv("YMS_BN_FIN_1024")) : 0;   // dev A/B
   // (tried: float4 channel quads x 32 row lanes with every load of a lane in flight at once --
   // the step got slower, 19.42 -> 19.65 ms interleaved; the finalize is not load-latency bound)
-  if (wide)
+  static const int v2 = getenv("YMS_BN_FIN_V2") ? atoi(getenv("YMS_BN_FIN_V2")) : 0;   // dev A/B
+  if (v2)
+    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(cdiv(c, 8)), dim3(256), 0, (hipStream_t)stream, c, ws, rows,
+                       count, dgamma, dbeta, coef);
+  else if (wide)
     hipLaunchKernelGGL(bn_bwd_finalize_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, ws,
                        rows, count, dgamma, dbeta, coef);
   else
