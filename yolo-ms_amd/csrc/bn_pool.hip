@@ -828,7 +828,12 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
 // blocks
 static long elem_ppb(long npix, int c, int iters = 4) {
   const long py = 256 / ((c + 7) / 8);
-  const long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * iters), 1), 8192);
+  long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * iters), 1), 8192);
+  // small layers (20^2 / 40^2 maps): at four iterations per thread they launch 100-400 blocks,
+  // 1-2 per CU, too few waves in flight for an HBM-bound pass; keep at least `minb` blocks while
+  // each thread still gets one full U-pixel iteration (YMS_BN_MINB, dev A/B)
+  static const long minb = getenv("YMS_BN_MINB") ? atol(getenv("YMS_BN_MINB")) : 0;
+  if (minb > 0) blocks = std::max<long>(blocks, std::min<long>(minb, cdiv(npix, py * BN_U)));
   return (npix + blocks - 1) / blocks;
 }
 
