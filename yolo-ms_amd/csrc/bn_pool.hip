@@ -168,6 +168,59 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* s
   }
 }
 
+// Forward finalize for tables of <= 1024 rows (rs == 1), latency-shaped: 8 channels x 32 row
+// lanes (256 threads), each lane issues the loads of up to 8 rows at a time (24 in flight) and
+// folds them with the same shifted fp64 update; a 5-level fixed-order tree over the lanes (the
+// 1024-thread kernel above runs a 7-level tree with two barriers per level).  In the forward no
+// side-stream work competes for CU slots, so the finalize's latency is the step's.  Measured
+// step-neutral to slightly faster (YOLOv8-s 18.71 / 18.71 -> 18.67 / 18.74 ms, YOLO-MS-S 37.29 /
+// 37.37 -> 37.24 / 37.26 ms, profiles/r03u_bn_finalize_small_ab.txt); YMS_BN_FIN_SMALL=0 restores.
+constexpr int FIN3_RL = 32;
+__global__ __launch_bounds__(256) void bn_finalize_small_kernel(int c, const float* stats, int rows, int ld,
+                                                                long count, const float* g, const float* b, float* rm,
+                                                                float* rv, float momentum, float eps, float* mi,
+                                                                float* scale, float* shift) {
+  __shared__ double red[FIN3_RL * 9][4];
+  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
+  const int ch = blockIdx.x * 8 + tx;
+  const float* cnt = stats + (long)rows * 2 * ld;
+  Moments a;
+  if (ch < c) {
+    for (int r0 = ty; r0 < rows; r0 += FIN3_RL * 8) {
+      float s1[8], m2[8], n[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int r = r0 + FIN3_RL * u;
+        const bool ok = r < rows;
+        s1[u] = ok ? stats[(long)r * 2 * ld + ch] : 0.f;
+        m2[u] = ok ? stats[(long)r * 2 * ld + ld + ch] : 0.f;
+        n[u] = ok ? cnt[r] : 0.f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) a.add_row(s1[u], m2[u], n[u]);
+    }
+  }
+  for (int h = FIN3_RL / 2; h >= 1; h >>= 1) {
+    if (ty >= h && ty < 2 * h) a.store(red, ty * 9 + tx);
+    __syncthreads();
+    if (ty < h) a.merge(Moments::load(red, (ty + h) * 9 + tx));
+    __syncthreads();
+  }
+  if (ty == 0 && ch < c) {
+    const double mean = a.n > 0.0 ? a.sum() / a.n : 0.0;
+    const double var = fmax(a.m2(), 0.0) / (double)count;
+    const float invstd = (float)(1.0 / sqrt(var + (double)eps));
+    const double uvar = count > 1 ? var * (double)count / (double)(count - 1) : var;
+    if (rm) rm[ch] = (float)((1.0 - momentum) * (double)rm[ch] + momentum * mean);
+    if (rv) rv[ch] = (float)((1.0 - momentum) * (double)rv[ch] + momentum * uvar);
+    mi[ch] = (float)mean;
+    mi[c + ch] = invstd;
+    const float sc = g[ch] * invstd;
+    scale[ch] = sc;
+    shift[ch] = b[ch] - (float)mean * sc;
+  }
+}
+
 // ------------------------------------------------------------------------------------------
 // Channel-stationary mapping for the per-channel elementwise / reduction kernels:
 // G = ceil(C/8) 16-B channel groups, thread (py, g) = (tid / G, tid % G) keeps the same
@@ -816,6 +869,13 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
     nrows = cdiv(rows, rs);
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(cdiv(c, 64), nrows), dim3(256), 0, (hipStream_t)stream, c,
                        stats, rows, stats_ld, rs);
+  }
+  static const int small = getenv("YMS_BN_FIN_SMALL") ? atoi(getenv("YMS_BN_FIN_SMALL")) : 1;   // dev A/B
+  if (small && rs == 1) {
+    hipLaunchKernelGGL(bn_finalize_small_kernel, dim3(cdiv(c, 8)), dim3(256), 0, (hipStream_t)stream, c,
+                       (const float*)stats, rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps,
+                       mean_invstd, scale, shift);
+    return launch_status();
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, FIN_CW)), dim3(1024), 0, (hipStream_t)stream, c,
                      (const float*)stats, nrows, stats_ld, rs, rows, count, gamma, beta, rmean, rvar, momentum,
