@@ -163,3 +163,34 @@ def _flat(st, cnt):
     base = st.reshape(-1)
     assert cnt.data_ptr() == base.data_ptr() + base.numel() * 4
     return torch.as_strided(base, (base.numel() + cnt.numel(),), (1,))
+
+
+# SPPF pool backward: the whole-map fused kernel (argmax + gather in LDS, one launch per pool) must
+# reproduce the two-kernel path bit for bit -- ties (quantised values), NaNs, map sizes of every
+# channel-group width (<= 400, <= 800, <= 1600 pixels), channel counts not a multiple of the group
+@pytest.mark.parametrize("n,h,w,c", [(2, 20, 20, 64), (1, 13, 17, 40), (2, 24, 30, 48), (1, 40, 40, 24),
+                                     (3, 5, 7, 16)])
+@pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
+def test_sppf_pool_bwd_fused_matches_two_kernel(n, h, w, c, dt, monkeypatch):
+    g = torch.Generator().manual_seed(n * 100 + h + w + c)
+    ld = 4 * c + 8
+    # slots 0..3 of an NHWC concat buffer at channel offset 8; quantised values give many ties
+    buf = torch.zeros(n, h, w, ld)
+    x0 = (torch.randint(-4, 5, (n, h, w, c), generator=g).float() * 0.25)
+    x0[0, 1, 2, :3] = float("nan")
+    buf[..., 8:8 + c] = x0
+    buf = buf.to(dt).cuda()
+    L.call("yms_sppf_pool_fwd", L.dtype_code(dt), n, h, w, c, buf.data_ptr(), ld, 8, L.stream_ptr())
+    g0 = torch.randn(n, h, w, ld, generator=g).to(dt).cuda()
+    ws = torch.empty(n * h * w * ((c + 7) // 8) * 8, dtype=torch.uint8, device="cuda")
+    outs = []
+    for fused in ("0", "1"):
+        monkeypatch.setenv("YMS_SPPF_FUSED", fused)
+        gb = g0.clone()
+        L.call("yms_sppf_pool_bwd", L.dtype_code(dt), n, h, w, c, buf.data_ptr(), ld, 8, gb.data_ptr(), ld, 8,
+               ws.data_ptr(), L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(gb.float().cpu())
+    a, b = outs
+    assert torch.equal(torch.isnan(a), torch.isnan(b))
+    assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))

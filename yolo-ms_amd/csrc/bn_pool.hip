@@ -704,6 +704,90 @@ __global__ void pool5_gather_kernel(int n, int h, int w, int c, const uint8_t* a
 }
 
 // ------------------------------------------------------------------------------------------
+// SPPF pool backward, one launch per chained pool (maps of <= 1600 pixels: the 20^2 / 40^2 SPPF of
+// a 640 / 1280 input): a block owns one image x CG channels of the whole map, stages the pool's
+// input slot and the output-gradient slot in LDS, forms every output's window argmax there (the
+// loop of pool5_argmax_kernel: first maximum in row-major window order, NaN wins) and gathers
+// each input pixel's gradient from the 5 x 5 outputs that chose it, in the order of
+// pool5_gather_kernel -- the same argmax bytes and the same fp32 sums (bit-identical), one global
+// pass over the three slots instead of 25 scattered L2 loads per element in each of two launches.
+// Opt-in (see yms_sppf_pool_bwd): measured slower inside the training step.
+// ------------------------------------------------------------------------------------------
+template <typename T, int CG>
+__global__ __launch_bounds__(256) void pool5_bwd_fused_kernel(int h, int w, int c, const T* buf, int ld, int in_off,
+                                                              T* g, int gy_off, int gx_off) {
+  constexpr int NCH = CG / 8;                     // 16-B chunks per pixel in the block
+  extern __shared__ __attribute__((aligned(16))) char dsm[];
+  const int hw = h * w;
+  Raw8<T>* X = reinterpret_cast<Raw8<T>*>(dsm);
+  Raw8<T>* GY = X + hw * NCH;
+  uint8_t* ARG = reinterpret_cast<uint8_t*>(GY + hw * NCH);
+  const int b = blockIdx.x, c0 = blockIdx.y * CG;
+  const long img = (long)b * hw;
+  for (int it = threadIdx.x; it < hw * NCH; it += 256) {
+    const int pix = it / NCH, j = it - pix * NCH, cc = c0 + 8 * j;
+    const int nv = min(8, c - cc);
+    if (nv > 0) {
+      load_raw8(buf + (img + pix) * ld + in_off + cc, nv, X[it]);
+      load_raw8(g + (img + pix) * ld + gy_off + cc, nv, GY[it]);
+    }
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < hw * NCH; it += 256) {
+    const int pix = it / NCH, j = it - pix * NCH;
+    const int y = pix / w, x = pix - y * w;
+    float best[8];
+    uint8_t idx[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; idx[i] = 255; }
+    for (int ky = 0; ky < 5; ++ky) {
+      const int yy = y - 2 + ky;
+      if (yy < 0 || yy >= h) continue;
+      for (int kx = 0; kx < 5; ++kx) {
+        const int xx = x - 2 + kx;
+        if (xx < 0 || xx >= w) continue;
+        float v[8];
+        unpack8(X[(yy * w + xx) * NCH + j], v);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (idx[i] == 255 || v[i] > best[i] || v[i] != v[i]) {  // (val > maxval) || isnan(val)
+            best[i] = v[i];
+            idx[i] = (uint8_t)(ky * 5 + kx);
+          }
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) ARG[it * 8 + i] = idx[i];
+  }
+  __syncthreads();
+  for (int it = threadIdx.x; it < hw * NCH; it += 256) {
+    const int pix = it / NCH, j = it - pix * NCH, cc = c0 + 8 * j;
+    const int nv = min(8, c - cc);
+    if (nv <= 0) continue;
+    const int y = pix / w, x = pix - y * w;
+    T* dst = g + (img + pix) * ld + gx_off + cc;
+    float acc[8];
+    load8(dst, nv, acc);
+    for (int ky = 0; ky < 5; ++ky) {
+      const int oy = y - ky + 2;
+      if (oy < 0 || oy >= h) continue;
+      for (int kx = 0; kx < 5; ++kx) {
+        const int ox = x - kx + 2;
+        if (ox < 0 || ox >= w) continue;
+        const int o = (oy * w + ox) * NCH + j;
+        const uint8_t want = (uint8_t)(ky * 5 + kx);
+        float gv[8];
+        unpack8(GY[o], gv);
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          if (ARG[o * 8 + i] == want) acc[i] += gv[i];
+      }
+    }
+    store8(dst, nv, acc);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // nearest x2 upsample
 // ------------------------------------------------------------------------------------------
 template <typename T>
@@ -1052,6 +1136,36 @@ yms_status yms_sppf_pool_bwd(int dtype, int n, int h, int w, int c, const void* 
   const long items = (long)n * h * w * ((c + 7) / 8);
   if (items >= (1l << 31)) return YMS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
+  // whole-map fused kernel: CG channels per block so the three LDS images fit 64 KB
+  const int hw = h * w;
+  const int cg = hw <= 400 ? 32 : (hw <= 800 ? 16 : (hw <= 1600 ? 8 : 0));
+  // opt-in (YMS_SPPF_FUSED=1, read per call): bit-identical but slower inside the overlapped step,
+  // YOLOv8-s 18.37 / 18.47 -> 18.51 / 18.57 ms (profiles/r03v_sppf_fused_ab.txt): its 64 KB-LDS blocks
+  // wait for LDS the side stream's weight-gradient blocks hold
+  const int fused_on = getenv("YMS_SPPF_FUSED") ? atoi(getenv("YMS_SPPF_FUSED")) : 0;
+  if (fused_on && cg > 0 && dtype != YMS_F32) {
+    const size_t lds = (size_t)hw * cg * (2 + 2 + 1);
+    const dim3 grid((unsigned)n, (unsigned)((c + cg - 1) / cg));
+    for (int k = 3; k >= 1; --k) {
+      const int in_off = off + (k - 1) * c, gy_off = goff + k * c, gx_off = goff + (k - 1) * c;
+      if (dtype == YMS_BF16) {
+        if (cg == 32) hipLaunchKernelGGL((pool5_bwd_fused_kernel<bf16, 32>), grid, dim3(256), lds, st, h, w, c,
+                                         (const bf16*)buf, ld, in_off, (bf16*)gbuf, gy_off, gx_off);
+        else if (cg == 16) hipLaunchKernelGGL((pool5_bwd_fused_kernel<bf16, 16>), grid, dim3(256), lds, st, h, w, c,
+                                              (const bf16*)buf, ld, in_off, (bf16*)gbuf, gy_off, gx_off);
+        else hipLaunchKernelGGL((pool5_bwd_fused_kernel<bf16, 8>), grid, dim3(256), lds, st, h, w, c,
+                                (const bf16*)buf, ld, in_off, (bf16*)gbuf, gy_off, gx_off);
+      } else {
+        if (cg == 32) hipLaunchKernelGGL((pool5_bwd_fused_kernel<f16, 32>), grid, dim3(256), lds, st, h, w, c,
+                                         (const f16*)buf, ld, in_off, (f16*)gbuf, gy_off, gx_off);
+        else if (cg == 16) hipLaunchKernelGGL((pool5_bwd_fused_kernel<f16, 16>), grid, dim3(256), lds, st, h, w, c,
+                                              (const f16*)buf, ld, in_off, (f16*)gbuf, gy_off, gx_off);
+        else hipLaunchKernelGGL((pool5_bwd_fused_kernel<f16, 8>), grid, dim3(256), lds, st, h, w, c,
+                                (const f16*)buf, ld, in_off, (f16*)gbuf, gy_off, gx_off);
+      }
+    }
+    return launch_status();
+  }
   for (int k = 3; k >= 1; --k) {
     // pool k reads slot k-1 (value buf) and produced slot k; push grad of slot k into slot k-1
     YMS_DT_DISPATCH(dtype, T, {
