@@ -988,7 +988,11 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   if (npix <= 0 || !z || !y || !vok(z_ld, z_off, c) || !vok(y_ld, y_off, c)) return YMS_ERR_INVALID;
   if (res && !vok(res_ld, res_off, c)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  const long ppb = elem_ppb(npix, c);
+  // two U-pixel iterations per thread: the forward affine pass (no side-stream work beside it) took
+  // 1.73 / 1.74 ms per YOLOv8-s step against 1.80 / 1.80 at four, 3.66-3.68 vs 3.70-3.73 ms on
+  // YOLO-MS-S (interleaved, profiles/r03y_affine_iters_ab.txt); YMS_BN_AFFINE_ITERS overrides
+  static const int iters = getenv("YMS_BN_AFFINE_ITERS") ? std::max(1, atoi(getenv("YMS_BN_AFFINE_ITERS"))) : 2;
+  const long ppb = elem_ppb(npix, c, iters);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
   YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(affine_act_kernel<T>, dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
