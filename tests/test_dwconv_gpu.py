@@ -88,7 +88,9 @@ def test_dwconv_fwd_dgrad_wgrad(shp, dt, tx, monkeypatch):
     _close(dw.cpu() - 0.5, wg.grad, 1e-4 if dt == "f32" else 2e-3)
 
 
-def test_add_views():
+@pytest.mark.parametrize("iters", ["0", "1", "2", "4"])
+def test_add_views(iters, monkeypatch):
+    monkeypatch.setenv("YMS_ADD_ITERS", iters)      # items per thread (read per call)
     g = torch.Generator().manual_seed(3)
     a = torch.randn(2, 24, 5, 7, generator=g)
     b = torch.randn(2, 24, 5, 7, generator=g)
@@ -103,9 +105,11 @@ def test_add_views():
     assert torch.equal(nchw(y, 24).cpu(), a.to(torch.bfloat16).float())
 
 
+@pytest.mark.parametrize("iters", ["0", "1", "2", "4"])
 @pytest.mark.parametrize("acc1,acc2", [(0, 0), (1, 0), (0, 1), (1, 1)])
-def test_add_grad2_routes_into_both_addends(acc1, acc2):
+def test_add_grad2_routes_into_both_addends(acc1, acc2, iters, monkeypatch):
     """yms_add_grad2: the MS-Block branch-sum backward, ga (+)= g and gb (+)= g in one pass."""
+    monkeypatch.setenv("YMS_ADD_ITERS", iters)
     g = torch.Generator().manual_seed(acc1 * 2 + acc2)
     npix, c = 3001, 24
     gy = torch.randn(npix, 40, generator=g).to(torch.bfloat16).cuda()          # a 40-wide buffer, slot at 8

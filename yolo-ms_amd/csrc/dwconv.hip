@@ -1054,43 +1054,102 @@ static int dw_wgrad_blocks(const yms_dw_shape* s) {
   } while (0)
 
 // y (+)= a + b over npix x c (b may be NULL): the MS-Block branch sum (X_i + Y_{i-1}) and, with
-// b = NULL, its backward (each addend's gradient (+)= the sum's gradient)
-template <typename T>
+// b = NULL, its backward (each addend's gradient (+)= the sum's gradient).  U = 16-B items per
+// thread, all loads issued before the first store (U = 0: grid-stride loop, one item at a time).
+template <typename T, int U>
 __global__ __launch_bounds__(256) void add_views_kernel(long items, int cg, const T* a, int a_ld, int a_off,
                                                         const T* b, int b_ld, int b_off, T* y, int y_ld, int y_off,
                                                         int accumulate) {
-  for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
-    const long pix = it / cg;
-    const int c = (int)(it - pix * cg) * 8;
-    float va[8], vb[8], vy[8];
-    Vec8<T>::load(a + pix * a_ld + a_off + c, va);
-    if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb);
-    if (accumulate) Vec8<T>::load(y + pix * y_ld + y_off + c, vy);
+  if constexpr (U == 0) {
+    for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
+      const long pix = it / cg;
+      const int c = (int)(it - pix * cg) * 8;
+      float va[8], vb[8], vy[8];
+      Vec8<T>::load(a + pix * a_ld + a_off + c, va);
+      if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb);
+      if (accumulate) Vec8<T>::load(y + pix * y_ld + y_off + c, vy);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) va[k] = (b ? va[k] + vb[k] : va[k]) + (accumulate ? vy[k] : 0.0f);
-    Vec8<T>::store(y + pix * y_ld + y_off + c, va);
+      for (int k = 0; k < 8; ++k) va[k] = (b ? va[k] + vb[k] : va[k]) + (accumulate ? vy[k] : 0.0f);
+      Vec8<T>::store(y + pix * y_ld + y_off + c, va);
+    }
+  } else {
+    const long base = blockIdx.x * (256l * U) + threadIdx.x;
+    float va[U][8], vb[U][8], vy[U][8];
+    long yo[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long it = base + u * 256l;
+      yo[u] = -1;
+      if (it < items) {
+        const long pix = it / cg;
+        const int c = (int)(it - pix * cg) * 8;
+        yo[u] = pix * y_ld + y_off + c;
+        Vec8<T>::load(a + pix * a_ld + a_off + c, va[u]);
+        if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb[u]);
+        if (accumulate) Vec8<T>::load(y + yo[u], vy[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (yo[u] < 0) continue;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) va[u][k] = (b ? va[u][k] + vb[u][k] : va[u][k]) + (accumulate ? vy[u][k] : 0.0f);
+      Vec8<T>::store(y + yo[u], va[u]);
+    }
   }
 }
 
-// Backward of y = a + b: g -> ga (+)= g and gb (+)= g in one pass (g read once)
-template <typename T>
+// Backward of y = a + b: g -> ga (+)= g and gb (+)= g in one pass (g read once); U as above
+template <typename T, int U>
 __global__ __launch_bounds__(256) void add_grad2_kernel(long items, int cg, const T* g, int g_ld, int g_off, T* y1,
                                                         int ld1, int off1, int acc1, T* y2, int ld2, int off2,
                                                         int acc2) {
-  for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
-    const long pix = it / cg;
-    const int c = (int)(it - pix * cg) * 8;
-    float vg[8], v1[8], v2[8];
-    Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
-    if (acc1) Vec8<T>::load(y1 + pix * ld1 + off1 + c, v1);
-    if (acc2) Vec8<T>::load(y2 + pix * ld2 + off2 + c, v2);
+  if constexpr (U == 0) {
+    for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
+      const long pix = it / cg;
+      const int c = (int)(it - pix * cg) * 8;
+      float vg[8], v1[8], v2[8];
+      Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
+      if (acc1) Vec8<T>::load(y1 + pix * ld1 + off1 + c, v1);
+      if (acc2) Vec8<T>::load(y2 + pix * ld2 + off2 + c, v2);
 #pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      v1[k] = acc1 ? v1[k] + vg[k] : vg[k];
-      v2[k] = acc2 ? v2[k] + vg[k] : vg[k];
+      for (int k = 0; k < 8; ++k) {
+        v1[k] = acc1 ? v1[k] + vg[k] : vg[k];
+        v2[k] = acc2 ? v2[k] + vg[k] : vg[k];
+      }
+      Vec8<T>::store(y1 + pix * ld1 + off1 + c, v1);
+      Vec8<T>::store(y2 + pix * ld2 + off2 + c, v2);
     }
-    Vec8<T>::store(y1 + pix * ld1 + off1 + c, v1);
-    Vec8<T>::store(y2 + pix * ld2 + off2 + c, v2);
+  } else {
+    const long base = blockIdx.x * (256l * U) + threadIdx.x;
+    float vg[U][8], v1[U][8], v2[U][8];
+    long o1[U], o2[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long it = base + u * 256l;
+      o1[u] = -1;
+      o2[u] = 0;
+      if (it < items) {
+        const long pix = it / cg;
+        const int c = (int)(it - pix * cg) * 8;
+        o1[u] = pix * ld1 + off1 + c;
+        o2[u] = pix * ld2 + off2 + c;
+        Vec8<T>::load(g + pix * g_ld + g_off + c, vg[u]);
+        if (acc1) Vec8<T>::load(y1 + o1[u], v1[u]);
+        if (acc2) Vec8<T>::load(y2 + o2[u], v2[u]);
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (o1[u] < 0) continue;
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        v1[u][k] = acc1 ? v1[u][k] + vg[u][k] : vg[u][k];
+        v2[u][k] = acc2 ? v2[u][k] + vg[u][k] : vg[u][k];
+      }
+      Vec8<T>::store(y1 + o1[u], v1[u]);
+      Vec8<T>::store(y2 + o2[u], v2[u]);
+    }
   }
 }
 
@@ -1320,16 +1379,32 @@ yms_status yms_dwconv_wgrad_bnin(const yms_dw_shape* s, const void* z, int z_ld,
                        stream);
 }
 
+// 16-B items per thread of the branch-sum kernels (YMS_ADD_ITERS: 0 = grid-stride loop over at most
+// 16384 blocks, 1, 2, 4; read per call)
+static int add_iters() {
+  const char* e = getenv("YMS_ADD_ITERS");
+  return e ? std::max(0, atoi(e)) : 0;
+}
+static unsigned add_grid(long items, int u) {
+  return u == 0 ? (unsigned)std::min<long>((items + 255) / 256, 16384) : (unsigned)((items + 256l * u - 1) / (256l * u));
+}
+
 yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,
                          int b_off, void* y, int y_ld, int y_off, int accumulate, void* stream) {
   if (npix <= 0 || c <= 0 || c % 8 || !a || !y || !dw_view_ok(a_ld, a_off, c) || !dw_view_ok(y_ld, y_off, c))
     return YMS_ERR_INVALID;
   if (b && !dw_view_ok(b_ld, b_off, c)) return YMS_ERR_INVALID;
   const long items = npix * (c / 8);
-  const unsigned grid = (unsigned)std::min<long>((items + 255) / 256, 16384);
-  YMS_DW_T(dtype, hipLaunchKernelGGL(add_views_kernel<TT>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, c / 8,
-                                     (const TT*)a, a_ld, a_off, (const TT*)b, b_ld, b_off, (TT*)y, y_ld, y_off,
-                                     accumulate));
+  const int u = add_iters();
+#define YMS_ADDV(UU)                                                                                             \
+  YMS_DW_T(dtype, hipLaunchKernelGGL((add_views_kernel<TT, UU>), dim3(add_grid(items, UU)), dim3(256), 0,          \
+                                     (hipStream_t)stream, items, c / 8, (const TT*)a, a_ld, a_off, (const TT*)b, b_ld, \
+                                     b_off, (TT*)y, y_ld, y_off, accumulate))
+  if (u == 0) YMS_ADDV(0);
+  else if (u == 1) YMS_ADDV(1);
+  else if (u == 2) YMS_ADDV(2);
+  else YMS_ADDV(4);
+#undef YMS_ADDV
   return launch_status();
 }
 
@@ -1339,9 +1414,16 @@ yms_status yms_add_grad2(int dtype, long npix, int c, const void* g, int g_ld, i
       !dw_view_ok(ld2, off2, c))
     return YMS_ERR_INVALID;
   const long items = npix * (c / 8);
-  const unsigned grid = (unsigned)std::min<long>((items + 255) / 256, 16384);
-  YMS_DW_T(dtype, hipLaunchKernelGGL(add_grad2_kernel<TT>, dim3(grid), dim3(256), 0, (hipStream_t)stream, items, c / 8,
-                                     (const TT*)g, g_ld, g_off, (TT*)y1, ld1, off1, acc1, (TT*)y2, ld2, off2, acc2));
+  const int u = add_iters();
+#define YMS_ADDG(UU)                                                                                            \
+  YMS_DW_T(dtype, hipLaunchKernelGGL((add_grad2_kernel<TT, UU>), dim3(add_grid(items, UU)), dim3(256), 0,         \
+                                     (hipStream_t)stream, items, c / 8, (const TT*)g, g_ld, g_off, (TT*)y1, ld1, off1, \
+                                     acc1, (TT*)y2, ld2, off2, acc2))
+  if (u == 0) YMS_ADDG(0);
+  else if (u == 1) YMS_ADDG(1);
+  else if (u == 2) YMS_ADDG(2);
+  else YMS_ADDG(4);
+#undef YMS_ADDG
   return launch_status();
 }
 
