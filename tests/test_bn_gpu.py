@@ -194,3 +194,41 @@ def test_sppf_pool_bwd_fused_matches_two_kernel(n, h, w, c, dt, monkeypatch):
     a, b = outs
     assert torch.equal(torch.isnan(a), torch.isnan(b))
     assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+
+
+@pytest.mark.parametrize("npix,c,ld,off", [(44800, 64, 64, 0), (40001, 24, 40, 8), (100, 16, 16, 0),
+                                           (25600, 768, 776, 8), (3001, 40, 48, 0), (999, 20, 32, 8),
+                                           (7 * 80 * 80, 128, 256, 128)])
+@pytest.mark.parametrize("dt", ["bf16", "f16", "f32"])
+@pytest.mark.parametrize("has_z", [True, False])
+def test_bn_bwd_reduce_pipelined_matches_serial(npix, c, ld, off, dt, has_z, monkeypatch):
+    """The software-pipelined reduce loop (c % 8 == 0, unconditional loads with the tail pixels
+    re-read and masked) sums in the serial loop's order; the two loops may contract a different
+    set of mul+add pairs into FMAs, so partial rows agree to fp32 rounding, not bit for bit."""
+    tdt, code = {"bf16": (torch.bfloat16, L.BF16), "f16": (torch.float16, L.F16), "f32": (torch.float32, L.F32)}[dt]
+    g = torch.Generator().manual_seed(npix * 7 + c)
+    z = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    gy = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    sc = (torch.rand(c, generator=g) + 0.5).cuda()
+    sh = (torch.randn(c, generator=g) * 0.2).cuda()
+    mi = torch.cat([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5]).cuda()
+    rows = L.lib().yms_bn_bwd_rows(npix, c)
+    outs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("YMS_BN_RED_PIPE", pipe)
+        ws = torch.full((rows + 4, 2, c), float("nan"), device="cuda")
+        L.call("yms_bn_act_bwd_reduce", code, npix, c, z.data_ptr() if has_z else None, ld, off, gy.data_ptr(), ld,
+               off, sc.data_ptr(), sh.data_ptr(), mi.data_ptr(), 1, ws.data_ptr(), L.stream_ptr())
+        torch.cuda.synchronize()
+        assert torch.isnan(ws[rows:]).all() and torch.isfinite(ws[:rows]).all()
+        outs.append(ws[:rows].cpu())
+    assert ((outs[0] - outs[1]).norm() / outs[0].norm()).item() < 1e-6
+    if has_z and dt == "f32":          # and the sums are the op's (fp64 reference of the same pixels)
+        zz, gg = z[:, off:off + c].double().cpu(), gy[:, off:off + c].double().cpu()
+        a = zz * sc.double().cpu() + sh.double().cpu()
+        s = torch.sigmoid(a)
+        da = gg * (s * (1 + a * (1 - s)))
+        xh = (zz - mi[:c].double().cpu()) * mi[c:].double().cpu()
+        tot = outs[1].double().sum(0)
+        assert ((tot[0] - da.sum(0)).norm() / da.sum(0).norm()).item() < 1e-5
+        assert ((tot[1] - (da * xh).sum(0)).norm() / (da * xh).sum(0).norm()).item() < 1e-5

@@ -301,7 +301,8 @@ struct BwdFin {          // fused finalize (FIN): the last reduce block to finis
   long count;
 };
 
-template <typename T, bool HAS_Z, bool FIN = false>
+// PIPE = false: the serial loop for every c (the default; YMS_BN_RED_PIPE=1 selects PIPE)
+template <typename T, bool HAS_Z, bool FIN = false, bool PIPE = true>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld,
                                                             int z_off, const T* gy, int gy_ld, int gy_off,
                                                             const float* scale, const float* shift,
@@ -322,35 +323,70 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
       load_params8(mi + c, c0, c, is, 0.f);
     }
     const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-    for (long base = p0 + m.py; base < p1; base += (long)m.PY * BN_U) {
-      Raw8<T> gr[BN_U], zr[BN_U];
+    auto accum = [&](const Raw8<T>& g, const Raw8<T>& zz) {
+      float gv[8], zv[8];
+      unpack8(g, gv);
+      if (HAS_Z) unpack8(zz, zv);
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long pix = base + (long)u * m.PY;
-        if (pix < p1) {
-          load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
-          if (HAS_Z) load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
+      for (int i = 0; i < 8; ++i) {
+        float da = gv[i], xh = 0.f;
+        if (HAS_Z) {
+          const float a = zv[i] * sc[i] + sh[i];
+          if (act == YMS_ACT_SILU) da = gv[i] * dsilu_f(a);
+          xh = (zv[i] - mu[i]) * is[i];
+        }
+        a1[i] += da;
+        a2[i] += da * xh;
+      }
+    };
+    const long step = (long)m.PY * BN_U;
+    if (PIPE && c % 8 == 0) {
+      // software-pipelined: the next U pixels' loads are in flight while this U's math runs
+      // (2 blocks per CU leave too few waves to hide HBM latency otherwise).  Loads are
+      // unconditional -- pixels past the range re-read the last one and are masked out of the
+      // sums -- so no branch separates a load from its wait and vmcnt can count.
+      auto issue = [&](long b, Raw8<T> (&g)[BN_U], Raw8<T> (&zz)[BN_U]) {
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u) {
+          const long pix = min(b + (long)u * m.PY, p1 - 1);
+          load_raw8(gy + pix * gy_ld + gy_off + c0, 8, g[u]);
+          if (HAS_Z) load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
+        }
+      };
+      auto consume = [&](long b, const Raw8<T> (&g)[BN_U], const Raw8<T> (&zz)[BN_U]) {
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u)
+          if (b + (long)u * m.PY < p1) accum(g[u], zz[u]);
+      };
+      long base = p0 + m.py;
+      if (base < p1) {
+        Raw8<T> ga[BN_U], za[BN_U], gb[BN_U], zb[BN_U];
+        issue(base, ga, za);
+        while (true) {
+          issue(base + step, gb, zb);
+          consume(base, ga, za);
+          base += step;
+          if (base >= p1) break;
+          issue(base + step, ga, za);
+          consume(base, gb, zb);
+          base += step;
+          if (base >= p1) break;
         }
       }
+    } else {
+      for (long base = p0 + m.py; base < p1; base += step) {
+        Raw8<T> gr[BN_U], zr[BN_U];
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
-        const long pix = base + (long)u * m.PY;
-        if (pix < p1) {
-          float gv[8], zv[8];
-          unpack8(gr[u], gv);
-          if (HAS_Z) unpack8(zr[u], zv);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            float da = gv[i], xh = 0.f;
-            if (HAS_Z) {
-              const float a = zv[i] * sc[i] + sh[i];
-              if (act == YMS_ACT_SILU) da = gv[i] * dsilu_f(a);
-              xh = (zv[i] - mu[i]) * is[i];
-            }
-            a1[i] += da;
-            a2[i] += da * xh;
+        for (int u = 0; u < BN_U; ++u) {
+          const long pix = base + (long)u * m.PY;
+          if (pix < p1) {
+            load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
+            if (HAS_Z) load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
           }
         }
+#pragma unroll
+        for (int u = 0; u < BN_U; ++u)
+          if (base + (long)u * m.PY < p1) accum(gr[u], zr[u]);
       }
     }
   }
@@ -1033,17 +1069,26 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
   const long ppb = bwd_pix_per_block(npix, c, false);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
+  // software-pipelined loop (c % 8 == 0), opt-in (YMS_BN_RED_PIPE=1, read per call): the reduce
+  // itself -10% / -9% (2.65 -> 2.40 ms per YOLOv8-s step, 6.48 -> 5.85 ms on YOLO-MS-S) but the
+  // apply after it +5% / +3% and the step unchanged (19.02 vs 19.09 ms, 37.55 vs 37.53 ms,
+  // interleaved, profiles/r03zb_bn_reduce_pipe_ab.txt): the step moves ~3.7 TB/s of HBM traffic
+  // on average, so a faster main-stream kernel hands the bandwidth to the side stream.
+  const char* pe = getenv("YMS_BN_RED_PIPE");
+  const bool pipe = pe && atoi(pe) != 0;
+#define YMS_RED(HZ, PP)                                                                                  \
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, HZ, false, PP>), dim3(rows), dim3(256), 0, \
+                                               (hipStream_t)stream, npix, c, HZ ? (const T*)z : (const T*)nullptr, \
+                                               HZ ? z_ld : 0, HZ ? z_off : 0, (const T*)gy, gy_ld, gy_off, scale,  \
+                                               shift, mean_invstd, act, ws, ppb))
   if (z) {
-    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, true>), dim3(rows), dim3(256), 0,
-                                                 (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
-                                                 (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd,
-                                                 act, ws, ppb));
+    if (pipe) YMS_RED(true, true);
+    else YMS_RED(true, false);
   } else {
-    YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, false>), dim3(rows), dim3(256), 0,
-                                                 (hipStream_t)stream, npix, c, (const T*)nullptr, 0, 0,
-                                                 (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd,
-                                                 act, ws, ppb));
+    if (pipe) YMS_RED(false, true);
+    else YMS_RED(false, false);
   }
+#undef YMS_RED
   return launch_status();
 }
 
