@@ -51,16 +51,16 @@ def test_host_shape_validation_and_sizes():
 
 def test_bn_bwd_rows_is_the_launched_block_count():
     """yms_bn_bwd_rows = the number of partial rows the (two-kernel) reduce writes: with
-    ppb = ceil(npix / min(512, ceil(npix/64))) the launch covers ceil(npix / ppb) blocks (the fused
+    ppb = ceil(npix / min(256, ceil(npix/64))) the launch covers ceil(npix / ppb) blocks (the fused
     reduce + finalize additionally caps rows at 32768 // c, never above this)."""
     for c in (8, 64, 80, 256, 512, 2048):
         for npix in (1, 63, 64, 65, 100, 32768, 32769, 40001, 44800, 57600, 63 * 640, 7 * 80 * 80, 64 * 160 * 160):
             rows = L.lib().yms_bn_bwd_rows(npix, c)
-            cap = max(1, min(512, (npix + 63) // 64))
+            cap = max(1, min(256, (npix + 63) // 64))
             ppb = -(-npix // cap)
             assert rows == -(-npix // ppb), (npix, c)
-            assert 1 <= rows <= 512 and (rows - 1) * ppb < npix <= rows * ppb, (npix, c)
-    assert L.lib().yms_bn_bwd_rows(44800, 64) == 510
+            assert 1 <= rows <= 256 and (rows - 1) * ppb < npix <= rows * ppb, (npix, c)
+    assert L.lib().yms_bn_bwd_rows(44801, 64) == 255      # below the cap: ppb 176
 
 
 def test_null_pointers_rejected_without_gpu():

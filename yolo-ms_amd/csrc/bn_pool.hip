@@ -301,7 +301,7 @@ struct BwdFin {          // fused finalize (FIN): the last reduce block to finis
   long count;
 };
 
-// PIPE = false: the serial loop for every c (the default; YMS_BN_RED_PIPE=1 selects PIPE)
+// PIPE = false: the serial loop for every c (YMS_BN_RED_PIPE=0, dev A/B)
 template <typename T, bool HAS_Z, bool FIN = false, bool PIPE = true>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld,
                                                             int z_off, const T* gy, int gy_ld, int gy_off,
@@ -1037,14 +1037,16 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   return launch_status();
 }
 
-// pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 512 (2 blocks
-// per CU leave room for the side-stream wgrad; interleaved A/B of the training step: cap 1024
-// 19.82 ms, 512 19.50 ms, 256 19.53 ms, 2048 20.33 ms; YMS_BN_BWD_ROWS_CAP overrides).  The fused
+// pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 256 with the
+// pipelined reduce loop (one block per CU; cap 128 / 256 / 384 / 512: 18.64 / 18.28 / 18.52 /
+// 18.74 ms per YOLOv8-s step, interleaved, profiles/r03ze_bn_reduce_pipe_cap_ab.txt).  With the
+// serial loop 512 was best (round 2: 1024 19.82 ms, 512 19.50, 256 19.53, 2048 20.33);
+// YMS_BN_BWD_ROWS_CAP overrides.  The fused
 // reduce + finalize (one last block sums the whole table) also keeps rows <= 32768 / c (table
 // <= 256 KB); the two-kernel path does not: that cap left 64-128 reduce blocks on 256 CUs for
 // the 256/512-channel layers (interleaved A/B: YOLOv8-s 19.51 -> 19.26 ms, -l 61.7 -> 60.9 ms).
 static long bwd_pix_per_block(long npix, int c, bool fused) {
-  static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 512;
+  static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 256;
   static const long cprod = getenv("YMS_BN_BWD_CCAP") ? atol(getenv("YMS_BN_BWD_CCAP")) : 32768;   // dev A/B
   const long ccap = (fused && cprod > 0) ? std::max(32l, cprod / std::max(c, 1)) : cap;
   const long rows = std::max(1l, std::min(std::min(cap, ccap), (npix + 63) / 64));
@@ -1052,7 +1054,7 @@ static long bwd_pix_per_block(long npix, int c, bool fused) {
 }
 
 // the number of partial rows the reduce WRITES = its launched block count ceil(npix / ppb).
-// Once a cap applies this can be below the cap (npix = 44800, c = 64: ppb 88, 510 blocks), so the
+// Once a cap applies this can be below the cap (npix = 44801, c = 64: ppb 176, 255 blocks), so the
 // scratch size, the launch and the finalize all use this one function.
 int yms_bn_bwd_rows(long npix, int c) {
   if (npix <= 0 || c <= 0) return 0;
@@ -1069,13 +1071,14 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
   const long ppb = bwd_pix_per_block(npix, c, false);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
-  // software-pipelined loop (c % 8 == 0), opt-in (YMS_BN_RED_PIPE=1, read per call): the reduce
-  // itself -10% / -9% (2.65 -> 2.40 ms per YOLOv8-s step, 6.48 -> 5.85 ms on YOLO-MS-S) but the
-  // apply after it +5% / +3% and the step unchanged (19.02 vs 19.09 ms, 37.55 vs 37.53 ms,
-  // interleaved, profiles/r03zb_bn_reduce_pipe_ab.txt): the step moves ~3.7 TB/s of HBM traffic
-  // on average, so a faster main-stream kernel hands the bandwidth to the side stream.
+  // software-pipelined loop (c % 8 == 0; YMS_BN_RED_PIPE=0 selects the serial loop, read per
+  // call).  At 512 rows it was step-neutral (the reduce -10%, the apply after it +5%,
+  // profiles/r03zb_bn_reduce_pipe_ab.txt); with the latency hidden inside each block, half the
+  // blocks (256 rows, bwd_pix_per_block) win: YOLOv8-s 18.63 -> 18.32 ms/step, YOLO-MS-S 37.42 ->
+  // 37.28 ms (means of four interleaved runs each, profiles/r03zd_*, r03ze_*); serial at 256
+  // rows is slower.
   const char* pe = getenv("YMS_BN_RED_PIPE");
-  const bool pipe = pe && atoi(pe) != 0;
+  const bool pipe = !pe || atoi(pe) != 0;
 #define YMS_RED(HZ, PP)                                                                                  \
   YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, HZ, false, PP>), dim3(rows), dim3(256), 0, \
                                                (hipStream_t)stream, npix, c, HZ ? (const T*)z : (const T*)nullptr, \
