@@ -232,3 +232,40 @@ def test_bn_bwd_reduce_pipelined_matches_serial(npix, c, ld, off, dt, has_z, mon
         tot = outs[1].double().sum(0)
         assert ((tot[0] - da.sum(0)).norm() / da.sum(0).norm()).item() < 1e-5
         assert ((tot[1] - (da * xh).sum(0)).norm() / (da * xh).sum(0).norm()).item() < 1e-5
+
+
+@pytest.mark.parametrize("npix,c,ld", [(44801, 64, 64), (3001, 40, 48), (25600, 768, 776), (999, 24, 32)])
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("gres_mode", [0, 1, 2])          # no residual gradient / store / accumulate
+@pytest.mark.parametrize("inplace", [False, True])         # dz written over z (the plan's default)
+@pytest.mark.parametrize("iters", ["4", "16"])
+def test_bn_bwd_apply_pipelined_matches_serial(npix, c, ld, dt, gres_mode, inplace, iters, monkeypatch):
+    """The software-pipelined apply loop (YMS_BN_APPLY_PIPE=1) against the serial loop: same dz and
+    residual gradient, including dz over z in place and an accumulated residual gradient (masked
+    stores: a clamped duplicate pixel is never written twice)."""
+    tdt, code = {"bf16": (torch.bfloat16, L.BF16), "f32": (torch.float32, L.F32)}[dt]
+    g = torch.Generator().manual_seed(npix + c + gres_mode)
+    z0 = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    gy = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    r0 = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    sc = (torch.rand(c, generator=g) + 0.5).cuda()
+    sh = (torch.randn(c, generator=g) * 0.2).cuda()
+    mi = torch.cat([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5]).cuda()
+    coef = (torch.randn(2 * c, generator=g) * 0.1).cuda()
+    monkeypatch.setenv("YMS_BN_APPLY_ITERS", iters)
+    outs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("YMS_BN_APPLY_PIPE", pipe)
+        z = z0.clone()
+        dz = z if inplace else torch.full_like(z0, 7.0)
+        r = r0.clone()
+        L.call("yms_bn_act_bwd_apply", code, npix, c, z.data_ptr(), ld, 0, gy.data_ptr(), ld, 0, sc.data_ptr(),
+               sh.data_ptr(), mi.data_ptr(), coef.data_ptr(), 1, dz.data_ptr(), ld, 0,
+               r.data_ptr() if gres_mode else None, ld, 0, int(gres_mode == 2), L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append((dz.float().cpu(), r.float().cpu()))
+    (d0, q0), (d1, q1) = outs
+    assert torch.equal(d0[:, c:], d1[:, c:]) and torch.equal(q0[:, c:], q1[:, c:])    # pad columns untouched
+    tol = 1e-6 if dt == "f32" else 1e-2
+    assert ((d0 - d1).abs().max() <= tol * (1 + d0.abs().max())).item()
+    assert torch.equal(q0, q1)           # the residual gradient is gy or r + gy: no FMA to contract

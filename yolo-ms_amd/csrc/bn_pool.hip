@@ -557,7 +557,11 @@ __global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(int c, const floa
   }
 }
 
-template <typename T>
+// PIPE (the default): software-pipelined like the reduce (c % 8 == 0): the next U pixels' loads (clamped to
+// the block's last pixel, masked) are in flight while this U is computed and stored.  Stores stay
+// masked: dz may overwrite z in place and gres may accumulate, so a duplicate pixel must not be
+// written twice.
+template <typename T, bool PIPE = false>
 __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, const T* z, int z_ld, int z_off,
                                                            const T* gy, int gy_ld, int gy_off, const float* scale,
                                                            const float* shift, const float* mi,
@@ -584,42 +588,82 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
     }
   }
   const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-  for (long base = p0 + m.py; base < p1; base += (long)m.PY * BN_U) {
-    Raw8<T> gr[BN_U], zr[BN_U], rr[BN_U];
+  const bool racc = gres && gres_acc;
+  auto emit = [&](long pix, const Raw8<T>& g, const Raw8<T>& zz, const Raw8<T>& rres, int valid) {
+    float gv[8], zv[8], out[8];
+    unpack8(g, gv);
+    unpack8(zz, zv);
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
-      const long pix = base + (long)u * m.PY;
-      if (pix < p1) {
-        load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
-        load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
-        if (gres && gres_acc) load_raw8(gres + pix * gres_ld + gres_off + c0, nv, rr[u]);
+    for (int i = 0; i < 8; ++i) {
+      float da = gv[i];
+      if (act == YMS_ACT_SILU) da *= dsilu_f(zv[i] * sc[i] + sh[i]);
+      out[i] = sc[i] * da + A[i] + Bz[i] * zv[i];
+    }
+    if (gres) {
+      float r[8];
+      if (gres_acc) {
+        unpack8(rres, r);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) r[i] += gv[i];
+        store8(gres + pix * gres_ld + gres_off + c0, valid, r);
+      } else {
+        store8(gres + pix * gres_ld + gres_off + c0, valid, gv);
       }
     }
+    store8(dz + pix * dz_ld + dz_off + c0, valid, out);
+  };
+  const long step = (long)m.PY * BN_U;
+  if (PIPE && c % 8 == 0) {
+    auto issue = [&](long b, Raw8<T> (&g)[BN_U], Raw8<T> (&zz)[BN_U], Raw8<T> (&rres)[BN_U]) {
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
-      const long pix = base + (long)u * m.PY;
-      if (pix < p1) {
-        float gv[8], zv[8], out[8];
-        unpack8(gr[u], gv);
-        unpack8(zr[u], zv);
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = min(b + (long)u * m.PY, p1 - 1);
+        load_raw8(gy + pix * gy_ld + gy_off + c0, 8, g[u]);
+        load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
+        if (racc) load_raw8(gres + pix * gres_ld + gres_off + c0, 8, rres[u]);
+      }
+    };
+    auto consume = [&](long b, const Raw8<T> (&g)[BN_U], const Raw8<T> (&zz)[BN_U], const Raw8<T> (&rres)[BN_U]) {
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float da = gv[i];
-          if (act == YMS_ACT_SILU) da *= dsilu_f(zv[i] * sc[i] + sh[i]);
-          out[i] = sc[i] * da + A[i] + Bz[i] * zv[i];
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = b + (long)u * m.PY;
+        if (pix < p1) emit(pix, g[u], zz[u], rres[u], 8);
+      }
+    };
+    long base = p0 + m.py;
+    if (base < p1) {
+      Raw8<T> ga[BN_U], za[BN_U], ra[BN_U], gb[BN_U], zb[BN_U], rb[BN_U];
+      issue(base, ga, za, ra);
+      // the next group's loads go out before this group's stores.  Every pixel is loaded and
+      // stored by one thread (in-place dz over z is per pixel and per thread); a clamped load of
+      // another thread's pixel may see its dz, but that value is masked and never stored
+      while (true) {
+        issue(base + step, gb, zb, rb);
+        consume(base, ga, za, ra);
+        base += step;
+        if (base >= p1) break;
+        issue(base + step, ga, za, ra);
+        consume(base, gb, zb, rb);
+        base += step;
+        if (base >= p1) break;
+      }
+    }
+  } else {
+    for (long base = p0 + m.py; base < p1; base += step) {
+      Raw8<T> gr[BN_U], zr[BN_U], rr[BN_U];
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = base + (long)u * m.PY;
+        if (pix < p1) {
+          load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
+          load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
+          if (racc) load_raw8(gres + pix * gres_ld + gres_off + c0, nv, rr[u]);
         }
-        if (gres) {
-          float r[8];
-          if (gres_acc) {
-            unpack8(rr[u], r);
+      }
 #pragma unroll
-            for (int i = 0; i < 8; ++i) r[i] += gv[i];
-            store8(gres + pix * gres_ld + gres_off + c0, nv, r);
-          } else {
-            store8(gres + pix * gres_ld + gres_off + c0, nv, gv);
-          }
-        }
-        store8(dz + pix * dz_ld + dz_off + c0, nv, out);
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = base + (long)u * m.PY;
+        if (pix < p1) emit(pix, gr[u], zr[u], rr[u], nv);
       }
     }
   }
@@ -1123,13 +1167,24 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
   if (!vok(z_ld, z_off, c) || !vok(gy_ld, gy_off, c) || !vok(dz_ld, dz_off, c)) return YMS_ERR_INVALID;
   if (gres && !vok(gres_ld, gres_off, c)) return YMS_ERR_INVALID;
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
-  static const int iters = getenv("YMS_BN_APPLY_ITERS") ? std::max(1, atoi(getenv("YMS_BN_APPLY_ITERS"))) : 4;
+  // software-pipelined loop at eight U-pixel iterations per thread (half the blocks of the serial
+  // loop's best, four): YOLO-MS-S 37.27 -> 37.11 ms/step, YOLOv8-s 18.53 -> 18.49 ms (means of
+  // two interleaved runs; 4 / 16 iterations pipelined are slower, profiles/r03zf_bn_apply_pipe_ab.txt).
+  // YMS_BN_APPLY_PIPE=0 selects the serial loop, YMS_BN_APPLY_ITERS overrides (both read per call).
+  const char* pe = getenv("YMS_BN_APPLY_PIPE");
+  const bool pipe = !pe || atoi(pe) != 0;
+  const char* ie = getenv("YMS_BN_APPLY_ITERS");
+  const int iters = ie ? std::max(1, atoi(ie)) : (pipe ? 8 : 4);
   const long ppb = elem_ppb(npix, c, iters);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(bn_bwd_apply_kernel<T>, dim3(blocks), dim3(256), 0,
-                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
-                                               (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd, coef,
-                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off, gres_acc, ppb));
+#define YMS_APPLY(PP)                                                                                        \
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PP>), dim3(blocks), dim3(256), 0,     \
+                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,        \
+                                               (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd, coef,  \
+                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off, gres_acc, ppb))
+  if (pipe) YMS_APPLY(true);
+  else YMS_APPLY(false);
+#undef YMS_APPLY
   return launch_status();
 }
 
