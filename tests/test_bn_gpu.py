@@ -269,3 +269,31 @@ def test_bn_bwd_apply_pipelined_matches_serial(npix, c, ld, dt, gres_mode, inpla
     tol = 1e-6 if dt == "f32" else 1e-2
     assert ((d0 - d1).abs().max() <= tol * (1 + d0.abs().max())).item()
     assert torch.equal(q0, q1)           # the residual gradient is gy or r + gy: no FMA to contract
+
+
+@pytest.mark.parametrize("npix,c,ld", [(44801, 64, 64), (3001, 40, 48), (25600, 768, 776), (999, 24, 32)])
+@pytest.mark.parametrize("dt", ["bf16", "f32"])
+@pytest.mark.parametrize("res_mode", [0, 1, 2])            # no residual / residual / y written over the residual
+@pytest.mark.parametrize("iters", ["2", "8"])
+def test_affine_act_pipelined_matches_serial(npix, c, ld, dt, res_mode, iters, monkeypatch):
+    """The software-pipelined forward BN+SiLU(+res) pass (YMS_BN_AFFINE_PIPE=1) against the
+    serial loop, ragged pixel counts and an in-place residual included."""
+    tdt, code = {"bf16": (torch.bfloat16, L.BF16), "f32": (torch.float32, L.F32)}[dt]
+    g = torch.Generator().manual_seed(npix + c + res_mode)
+    z = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    r0 = torch.randn(npix, ld, generator=g).to(tdt).cuda()
+    sc = (torch.rand(c, generator=g) + 0.5).cuda()
+    sh = (torch.randn(c, generator=g) * 0.2).cuda()
+    monkeypatch.setenv("YMS_BN_AFFINE_ITERS", iters)
+    outs = []
+    for pipe in ("0", "1"):
+        monkeypatch.setenv("YMS_BN_AFFINE_PIPE", pipe)
+        r = r0.clone()
+        y = r if res_mode == 2 else torch.full_like(z, 7.0)
+        L.call("yms_affine_act", code, npix, c, z.data_ptr(), ld, 0, sc.data_ptr(), sh.data_ptr(), 1,
+               r.data_ptr() if res_mode else None, ld, 0, y.data_ptr(), ld, 0, L.stream_ptr())
+        torch.cuda.synchronize()
+        outs.append(y.float().cpu())
+    assert torch.equal(outs[0][:, c:], outs[1][:, c:])
+    tol = 1e-6 if dt == "f32" else 1e-2
+    assert ((outs[0] - outs[1]).abs().max() <= tol * (1 + outs[0].abs().max())).item()

@@ -249,7 +249,9 @@ __device__ __forceinline__ void load_params8(const float* p, int c0, int c, floa
 // parallelism; these kernels are HBM-bound).
 constexpr int BN_U = 4;
 
-template <typename T>
+// PIPE (the default): software-pipelined (c % 8 == 0) like the backward passes: the next U pixels' loads
+// (clamped to the block's last pixel, masked) are in flight while this U is computed and stored.
+template <typename T, bool PIPE = false>
 __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const T* z, int z_ld, int z_off,
                                                          const float* scale, const float* shift, int act,
                                                          const T* res, int res_ld, int res_off, T* y,
@@ -261,31 +263,66 @@ __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const
   load_params8(scale, c0, c, sc, 1.0f);
   load_params8(shift, c0, c, sh, 0.0f);
   const long p0 = blockIdx.x * ppb, p1 = min(npix, p0 + ppb);
-  for (long base = p0 + m.py; base < p1; base += (long)m.PY * BN_U) {
-    Raw8<T> zr[BN_U], rr[BN_U];
+  auto emit = [&](long pix, const Raw8<T>& zz, const Raw8<T>& rres, int valid) {
+    float v[8], r[8];
+    unpack8(zz, v);
+    if (res) unpack8(rres, r);
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
-      const long pix = base + (long)u * m.PY;
-      if (pix < p1) {
-        load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
-        if (res) load_raw8(res + pix * res_ld + res_off + c0, nv, rr[u]);
+    for (int i = 0; i < 8; ++i) {
+      float a = v[i] * sc[i] + sh[i];
+      if (act == YMS_ACT_SILU) a = silu_f(a);
+      if (res) a += r[i];
+      v[i] = a;
+    }
+    store8(y + pix * y_ld + y_off + c0, valid, v);
+  };
+  const long step = (long)m.PY * BN_U;
+  if (PIPE && c % 8 == 0) {
+    auto issue = [&](long b, Raw8<T> (&zz)[BN_U], Raw8<T> (&rres)[BN_U]) {
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = min(b + (long)u * m.PY, p1 - 1);
+        load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
+        if (res) load_raw8(res + pix * res_ld + res_off + c0, 8, rres[u]);
+      }
+    };
+    auto consume = [&](long b, const Raw8<T> (&zz)[BN_U], const Raw8<T> (&rres)[BN_U]) {
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = b + (long)u * m.PY;
+        if (pix < p1) emit(pix, zz[u], rres[u], 8);
+      }
+    };
+    long base = p0 + m.py;
+    if (base < p1) {
+      Raw8<T> za[BN_U], ra[BN_U], zb[BN_U], rb[BN_U];
+      issue(base, za, ra);
+      while (true) {
+        issue(base + step, zb, rb);
+        consume(base, za, ra);
+        base += step;
+        if (base >= p1) break;
+        issue(base + step, za, ra);
+        consume(base, zb, rb);
+        base += step;
+        if (base >= p1) break;
       }
     }
+  } else {
+    for (long base = p0 + m.py; base < p1; base += step) {
+      Raw8<T> zr[BN_U], rr[BN_U];
 #pragma unroll
-    for (int u = 0; u < BN_U; ++u) {
-      const long pix = base + (long)u * m.PY;
-      if (pix < p1) {
-        float v[8], r[8];
-        unpack8(zr[u], v);
-        if (res) unpack8(rr[u], r);
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          float a = v[i] * sc[i] + sh[i];
-          if (act == YMS_ACT_SILU) a = silu_f(a);
-          if (res) a += r[i];
-          v[i] = a;
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = base + (long)u * m.PY;
+        if (pix < p1) {
+          load_raw8(z + pix * z_ld + z_off + c0, nv, zr[u]);
+          if (res) load_raw8(res + pix * res_ld + res_off + c0, nv, rr[u]);
         }
-        store8(y + pix * y_ld + y_off + c0, nv, v);
+      }
+#pragma unroll
+      for (int u = 0; u < BN_U; ++u) {
+        const long pix = base + (long)u * m.PY;
+        if (pix < p1) emit(pix, zr[u], rr[u], nv);
       }
     }
   }
@@ -1071,13 +1108,24 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   // two U-pixel iterations per thread: the forward affine pass (no side-stream work beside it) took
   // 1.73 / 1.74 ms per YOLOv8-s step against 1.80 / 1.80 at four, 3.66-3.68 vs 3.70-3.73 ms on
   // YOLO-MS-S (interleaved, profiles/r03y_affine_iters_ab.txt); YMS_BN_AFFINE_ITERS overrides
-  static const int iters = getenv("YMS_BN_AFFINE_ITERS") ? std::max(1, atoi(getenv("YMS_BN_AFFINE_ITERS"))) : 2;
+  // software-pipelined loop (the default; YMS_BN_AFFINE_PIPE=0 selects the serial loop): affine
+  // 1.72 -> 1.70 ms per YOLOv8-s step, 3.68 -> 3.57 ms on YOLO-MS-S, steps 18.20 -> 18.13 ms and
+  // 37.24 -> 37.12 ms (interleaved pairs; pipelined at 4 / 8 iterations slower,
+  // profiles/r03zg_affine_pipe_ab.txt).  Both knobs read per call.
+  const char* pe = getenv("YMS_BN_AFFINE_PIPE");
+  const bool pipe = !pe || atoi(pe) != 0;
+  const char* ie = getenv("YMS_BN_AFFINE_ITERS");
+  const int iters = ie ? std::max(1, atoi(ie)) : 2;
   const long ppb = elem_ppb(npix, c, iters);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL(affine_act_kernel<T>, dim3(blocks), dim3(256), 0,
-                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
-                                               scale, shift, act, (const T*)res, res_ld, res_off, (T*)y,
-                                               y_ld, y_off, ppb));
+#define YMS_AFF(PP)                                                                                  \
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((affine_act_kernel<T, PP>), dim3(blocks), dim3(256), 0, \
+                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off, \
+                                               scale, shift, act, (const T*)res, res_ld, res_off, (T*)y, \
+                                               y_ld, y_off, ppb))
+  if (pipe) YMS_AFF(true);
+  else YMS_AFF(false);
+#undef YMS_AFF
   return launch_status();
 }
 
