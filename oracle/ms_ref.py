@@ -1,15 +1,23 @@
 """CPU restatement of the YOLO-MS family (MS-Block / HKS) -- TEST INFRASTRUCTURE ONLY.
 
 Parity for this family is NOT reference-pinned: the reference repository contains no MS-Block
-code (annotations.md:66-133 is a diagram).  The structure restated here is the one
-SURVEY 7.4 specifies (YOLO-MS paper, arXiv 2308.05480), written independently of the product
-module (yolo-ms_amd/yolov8/model/yolo_ms.py) as plain functional torch-CPU fp32:
+code (annotations.md:66-133 is a diagram, model_zoos.md:21-53 the upstream size
+table).  The structure restated here is the one SURVEY 7.4 specifies (YOLO-MS paper, arXiv
+2308.05480) on the diagram's topology, written independently of the product module
+(yolo-ms_amd/yolov8/model/yolo_ms.py) as plain functional torch-CPU fp32:
 
   IB_k(x)      = SiLU(BN(conv1x1)) -> SiLU(BN(depthwise kxk, groups=2c)) -> SiLU(BN(conv1x1))
   MSBlock(x)   = conv1x1(cat[Y1, Y2, Y3]);  [X1|X2|X3] = conv1x1(x),  Y1 = X1,  Yi = IB^L(Xi + Y(i-1))
-  backbone     = YOLOv8 stem (yolov8_backbone.py:54-73) with C2f stage i -> MSBlock(k = 3, 5, 7, 9)
-  neck         = YOLOv8 PAFPN (yolov8_neck.py:67-94) with C2f -> MSBlock(k = 3)
-  head         = the reference head (model_ref.head_raw / decode, reference-pinned)
+  backbone     = conv0 s2, conv1 s2, MSBlock(k3), conv3 s2, MSBlock(k5) -> P3, conv5 s2,
+                 MSBlock(k7) -> P4, conv7 s2, MSBlock(k9), SPPF ("MS-SPPF") -> P5
+  neck         = PAFPN with MSFusion = 1x1 reduce of the deeper map, nearest x2, concat:
+                 r5 = reduce_5(P5); td4 = MSBlock(cat[up r5, P4]); r4 = reduce_4(td4);
+                 out1 = MSBlock(cat[up r4, P3]); out2 = MSBlock(cat[conv1 s2 out1, r4]);
+                 out3 = MSBlock(cat[conv2 s2 out2, r5])          (neck MSBlocks k = 3)
+  head         = the reference head (model_ref.head_raw / decode, reference-pinned) on the neck widths
+
+Widths per version (stem c1, stage c2..c5; IB layers per branch) are the build's calibration to
+model_zoos.md:21-53 (params / MACs at 640); ``complexity`` recounts both from this restatement.
 
 Only tests/ may import this module.
 """
@@ -23,14 +31,15 @@ import torch.nn.functional as F
 
 from oracle import model_ref as M
 
-VERSIONS = {"ms-xs": "n", "ms-s": "s", "ms-l": "l"}
+# version -> ((c1, c2, c3, c4, c5), IB layers per branch)
+VERSIONS = {"ms-xs": ((24, 48, 96, 192, 192), 2),
+            "ms-s": ((40, 80, 128, 256, 256), 2),
+            "ms-l": ((56, 112, 224, 448, 384), 2)}
 HKS = (3, 5, 7, 9)
 
 
 def params(version):
-    base = VERSIONS[version]
-    d, w, r = M.yolo_params(base)
-    return d, w, r, max(1, round(3 * d)), base
+    return VERSIONS[version]
 
 
 def _conv_keys(name, cin, cout, k, groups=1):
@@ -55,10 +64,20 @@ def _msblock_keys(name, cin, cout, k, L):
     return out
 
 
+def _head_keys(lvl_c, nc):
+    """yolov8_head.py:83-113 for explicit level widths (box hidden 64, cls hidden nc)."""
+    out = []
+    for br, hid in (("box", 64), ("cls", nc)):
+        for lv, c in enumerate(lvl_c):
+            out += _conv_keys(f"head.{br}.{lv}.0", c, hid, 3)
+            out += _conv_keys(f"head.{br}.{lv}.1", hid, hid, 3)
+            out += [(f"head.{br}.{lv}.2.weight", (hid, hid, 1, 1)), (f"head.{br}.{lv}.2.bias", (hid,))]
+    out.append(("head.dfl.conv.weight", (1, 16, 1, 1)))
+    return out
+
+
 def state_keys(version, nc):
-    d, w, r, L, base = params(version)
-    i = int
-    c1, c2, c3, c4, c5 = i(64 * w), i(128 * w), i(256 * w), i(512 * w), i(512 * w * r)
+    (c1, c2, c3, c4, c5), L = params(version)
     keys = []
     for name, ci, co in (("conv0", 3, c1), ("conv1", c1, c2), ("conv3", c2, c3), ("conv5", c3, c4), ("conv7", c4, c5)):
         keys += _conv_keys(f"backbone.{name}", ci, co, 3)
@@ -66,14 +85,42 @@ def state_keys(version, nc):
         keys += _msblock_keys(f"backbone.{name}", c, c, k, L)
     keys += _conv_keys("backbone.sppf.conv1", c5, c5 // 2, 1)
     keys += _conv_keys("backbone.sppf.conv2", (c5 // 2) * 4, c5, 1)
-    keys += _msblock_keys("neck.ms_1", i(512 * w * (1 + r)), i(512 * w), 3, L)
-    keys += _msblock_keys("neck.ms_2", i(768 * w), i(256 * w), 3, L)
-    keys += _msblock_keys("neck.ms_3", i(768 * w), i(512 * w), 3, L)
-    keys += _msblock_keys("neck.ms_4", i(512 * w * (1 + r)), i(512 * w * r), 3, L)
-    keys += _conv_keys("neck.conv1", i(256 * w), i(256 * w), 3)
-    keys += _conv_keys("neck.conv2", i(512 * w), i(512 * w), 3)
-    keys += [kv for kv in M.state_keys(base, nc) if kv[0].startswith("head.")]
+    keys += _conv_keys("neck.reduce_5", c5, c4, 1)
+    keys += _conv_keys("neck.reduce_4", c4, c3, 1)
+    keys += _msblock_keys("neck.ms_1", 2 * c4, c4, 3, L)
+    keys += _msblock_keys("neck.ms_2", 2 * c3, c3, 3, L)
+    keys += _msblock_keys("neck.ms_3", 2 * c3, c4, 3, L)
+    keys += _msblock_keys("neck.ms_4", 2 * c4, c5, 3, L)
+    keys += _conv_keys("neck.conv1", c3, c3, 3)
+    keys += _conv_keys("neck.conv2", c4, c4, 3)
+    keys += _head_keys((c3, c4, c5), nc)
     return keys
+
+
+def complexity(version, nc=80, size=640):
+    """-> (parameters excluding the frozen DFL projection, conv MACs per image at size x size),
+    counted by tracing this restatement's F.conv2d calls on the meta device."""
+    n_par = sum(math.prod(s) for k, s in state_keys(version, nc)
+                if not k.endswith(("running_mean", "running_var", "num_batches_tracked"))
+                and k != "head.dfl.conv.weight")
+    macs = 0
+    orig = F.conv2d
+
+    def hook(x, wt, b=None, stride=1, padding=0, dilation=1, groups=1):
+        nonlocal macs
+        y = orig(x, wt, b, stride, padding, dilation, groups)
+        if wt.shape[0] != 1 or wt.shape[1] != 16:      # not the DFL projection
+            macs += y.shape[1] * y.shape[2] * y.shape[3] * wt.shape[1] * wt.shape[2] * wt.shape[3]
+        return y
+
+    sd = {k: torch.zeros(s, device="meta") if len(s) else torch.zeros((), device="meta")
+          for k, s in state_keys(version, nc)}
+    F.conv2d = hook
+    try:
+        forward(sd, version, nc, torch.zeros(1, 3, size, size, device="meta"), True)
+    finally:
+        F.conv2d = orig
+    return n_par, macs
 
 
 def init_params(version, nc):
@@ -149,7 +196,7 @@ def msblock(p, name, x, k, L, training):
 
 
 def backbone(p, version, x, training):
-    L = params(version)[3]
+    L = params(version)[1]
     x = conv_block(p, "backbone.conv0", x, 3, 2, training)
     x = conv_block(p, "backbone.conv1", x, 3, 2, training)
     x = msblock(p, "backbone.ms_2", x, HKS[0], L, training)
@@ -163,19 +210,16 @@ def backbone(p, version, x, training):
     return out1, out2, out3
 
 
-def neck(p, version, x_res_1, x_res_2, x, training):
-    L = params(version)[3]
-    res_1 = x
-    x = torch.cat([M.upsample(x), x_res_2], 1)
-    res_2 = msblock(p, "neck.ms_1", x, 3, L, training)
-    x = torch.cat([M.upsample(res_2), x_res_1], 1)
-    out1 = msblock(p, "neck.ms_2", x, 3, L, training)
+def neck(p, version, p3, p4, p5, training):
+    L = params(version)[1]
+    r5 = conv_block(p, "neck.reduce_5", p5, 1, 1, training)
+    td4 = msblock(p, "neck.ms_1", torch.cat([M.upsample(r5), p4], 1), 3, L, training)
+    r4 = conv_block(p, "neck.reduce_4", td4, 1, 1, training)
+    out1 = msblock(p, "neck.ms_2", torch.cat([M.upsample(r4), p3], 1), 3, L, training)
     x = conv_block(p, "neck.conv1", out1, 3, 2, training)
-    x = torch.cat([x, res_2], 1)
-    out2 = msblock(p, "neck.ms_3", x, 3, L, training)
+    out2 = msblock(p, "neck.ms_3", torch.cat([x, r4], 1), 3, L, training)
     x = conv_block(p, "neck.conv2", out2, 3, 2, training)
-    x = torch.cat([x, res_1], 1)
-    out3 = msblock(p, "neck.ms_4", x, 3, L, training)
+    out3 = msblock(p, "neck.ms_4", torch.cat([x, r5], 1), 3, L, training)
     return out1, out2, out3
 
 

@@ -92,7 +92,17 @@ def _worker(rank, world, port, q):
         with torch.no_grad():
             m.running_mean.fill_(7.0 * (rank + 1))
         dp(torch.zeros(2, 4, 3, 3, dtype=torch.float64))
-        q.put((rank, ok_grad, launched, ok_bcast, (rm1, m.running_mean[0].item())))
+        # mixed buffer dtypes (no single flat tensor): a replaced buffer must still be the one synced
+        mm = torch.nn.Sequential(torch.nn.BatchNorm2d(4), torch.nn.BatchNorm2d(4).double())
+        dpm = DataParallel(mm, bucket_cap_mb=1.0)
+        mm[0].running_mean = torch.full((4,), 3.0 * (rank + 1))      # replaced after wrapping
+        with torch.no_grad():
+            mm[1].running_mean.fill_(2.0 * (rank + 1))
+        dpm.eval()
+        with torch.no_grad():
+            dpm._sync_buffers()
+        mixed = (mm[0].running_mean[0].item(), mm[1].running_mean[0].item())
+        q.put((rank, ok_grad, launched, ok_bcast, (rm1, m.running_mean[0].item()), mixed))
     finally:
         dist.destroy_process_group()
 
@@ -108,13 +118,14 @@ def test_bucketed_allreduce_gloo_world2():
     res = [q.get(timeout=120) for _ in range(world)]
     for p in procs:
         p.join(timeout=60)
-    for rank, ok_grad, launched, ok_bcast, rm in res:
+    for rank, ok_grad, launched, ok_bcast, rm, mixed in res:
         assert ok_grad, rank
         assert launched[0] == launched[1] >= 3, launched
         assert ok_bcast, rank
         # rank 0's buffer (5.0) broadcast before forward, then BN2d(momentum 0.1) on zeros
         assert abs(rm[0] - 0.9 * 5.0) < 1e-5, rm
         assert abs(rm[1] - 0.9 * 7.0) < 1e-5, rm     # rank 0's value after .double()
+        assert mixed == (3.0, 2.0), mixed              # rank 0's values, incl. the replaced buffer
 
 
 def test_bucket_layout_on_the_real_plan():

@@ -150,3 +150,49 @@ def test_loss_terms_are_reported_not_differentiable():
         terms[0].backward()
     total.backward()
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in preds)
+
+
+@pytest.mark.parametrize("name", [c for c in CASES if c != "posw"])
+def test_simplified_loss_dropin_vs_reference_fixtures(name):
+    """yolov8.tools.simplified_loss.SimplifiedYOLOLoss built with train.py:321-330's exact keyword set
+    (the reference's defaults for alpha / gamma / box_weight / cls_weight) runs ComputeLoss's CIoU
+    semantics: its total and terms and d(total)/d(maps) match the reference-generated fixtures."""
+    from yolov8.tools.simplified_loss import SimplifiedYOLOLoss
+    z = V.load_loss_case(name)
+    if "ciou" not in z["ious"]:
+        pytest.skip("fixture has no CIoU case")
+    bf16 = bool(z["bf16"][0])
+    dtype = torch.bfloat16 if bf16 else torch.float32
+    vtol, gtol = (1e-4, 4e-3) if bf16 else (2e-5, 2e-4)
+    img_h, img_w = z["img"]
+    crit = SimplifiedYOLOLoss(num_classes=z["nc"], device=DEV, img_size=(img_h, img_w),
+                              strides=[8., 16., 32.], alpha=0.25, gamma=1.5, box_weight=7.5, cls_weight=0.5)
+    preds = [_channels_last(torch.from_numpy(m), dtype).requires_grad_(True) for m in z["maps"]]
+    loss, items = crit(preds, torch.from_numpy(z["targets"]).to(DEV))
+    assert set(items) >= {"loss_box", "loss_cls", "loss_dfl"}
+    loss.backward()
+    vals = np.array([items["total_loss"], items["loss_box"], items["loss_cls"], items["loss_dfl"]])
+    assert abs(float(loss) - vals[0]) <= 1e-6 * max(1.0, abs(vals[0]))
+    check_against_fixture(z, "ciou", vals, [p.grad.float().cpu().double().numpy() for p in preds], vtol, gtol)
+
+
+def test_simplified_loss_weights_map_onto_terms():
+    """box_weight / cls_weight scale the box and classification terms (DFL keeps ComputeLoss's 1.5);
+    the terms themselves do not depend on the weights."""
+    from yolov8.tools.simplified_loss import SimplifiedYOLOLoss
+    z = V.load_loss_case("small")
+    img = z["img"]
+    tg = torch.from_numpy(z["targets"]).to(DEV)
+    outs = []
+    for bw, cw in ((7.5, 0.5), (2.0, 3.0)):
+        crit = SimplifiedYOLOLoss(z["nc"], DEV, img_size=img, box_weight=bw, cls_weight=cw)
+        preds = [_channels_last(torch.from_numpy(m), torch.float32).requires_grad_(True) for m in z["maps"]]
+        loss, items = crit(preds, tg)
+        loss.backward()
+        assert abs(items["total_loss"] - (bw * items["loss_box"] + cw * items["loss_cls"] + 1.5 * items["loss_dfl"])) \
+            <= 1e-5 * abs(items["total_loss"])
+        assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in preds)
+        outs.append(items)
+    a, b = outs
+    for k in ("loss_box", "loss_cls", "loss_dfl"):
+        assert abs(a[k] - b[k]) <= 1e-6 * max(abs(a[k]), 1e-3)

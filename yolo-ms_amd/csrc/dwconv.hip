@@ -921,9 +921,10 @@ static int dw_occ(const yms_dw_shape* s) {
 // per block, 512 threads) for k = 3 when C is a multiple of 64, else 4 (32 channels: the other half
 // of each line is read and written by another block at another time).  YMS_DW_G=4|8 forces (dev A/B).
 static int dw_fwd_g(const yms_dw_shape* s) {
+  const bool g8_ok = s->k == 3 && s->c % 64 == 0 && s->dtype != YMS_F32;
   const int f = dw_env("YMS_DW_G", 0);
-  if ((f == 4 || f == 8) && (f == 4 || s->k == 3)) return f;
-  return (s->k == 3 && s->c % 64 == 0 && s->dtype != YMS_F32) ? 8 : 4;
+  if (f == 4 || (f == 8 && g8_ok)) return f;   // the override never lifts the G = 8 path's conditions
+  return g8_ok ? 8 : 4;
 }
 
 // forward / dgrad grid: image column tiles split into strips of tps tiles.  The strip length is

@@ -150,7 +150,10 @@ _CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd"
 _DW = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad", "yms_dwconv_dgrad_bnred", "yms_dwconv_fwd_bnin",
        "yms_dwconv_wgrad_bnin")
 # launches whose hipStream_t is the last argument (status-returning entry points ending in a void*)
-_STREAM_LAST = {n for n, (res, args) in _SIGS.items() if res is _I and args and args[-1] is _P}
+# (host-only entry points whose last pointer is a host buffer are listed out explicitly)
+_HOST_ONLY = {"yms_map_accumulate", "yms_pack_job_init"}
+_STREAM_LAST = {n for n, (res, args) in _SIGS.items()
+                if res is _I and args and args[-1] is _P and n not in _HOST_ONLY}
 
 
 _FN = {}

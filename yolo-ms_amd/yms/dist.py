@@ -151,7 +151,9 @@ class DataParallel(nn.Module):
         return all(m._buffers.get(n) is not None and m._buffers[n].data_ptr() == p for m, n, p in self._views)
 
     def _sync_buffers(self):
-        if self._flat is not None and not self._flat_is_current():
+        if self._flat is None or not self._flat_is_current():
+            # mixed dtypes / devices keep per-buffer references: re-collect them from the module on
+            # every call, so a replaced buffer is never the one broadcast into
             self._flat_buffers()
         if self._flat is not None:
             dist.broadcast(self._flat, 0, group=self.group)

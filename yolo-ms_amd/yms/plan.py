@@ -384,7 +384,8 @@ class BiasConvOp:
             self.t_wp = La.alloc(self.wp_elems * es)
             self.t_wpt = La.alloc(self.wpt_elems * es)
             plan.need_scratch("bwd", 4 * 2 * self.c * L.lib().yms_bn_bwd_rows(self.npix, self.c))
-            plan.need_scratch("wgrad", L.lib().yms_conv_wgrad_ws_bytes(self.sp))
+            self.wg_ws = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
+            plan.need_scratch("wgrad", self.wg_ws)
             self.cnt = plan.counter()
 
     def prepare_eval(self, rt):
@@ -423,7 +424,7 @@ class BiasConvOp:
         dw = rt.pgrad(self.pw)
         if dw is not None:
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, gy, gyl, gyo,
-                   rt.gbase + rt.plan.gscratch["wgrad"], L.lib().yms_conv_wgrad_ws_bytes(self.sp), dw, 0, rt.wst())
+                   rt.gbase + rt.plan.gscratch["wgrad"], self.wg_ws, dw, 0, rt.wst())
 
     def grad_params(self):
         return [self.pbias, self.pw]
@@ -471,7 +472,10 @@ class DWConvOp(ConvOp):
             plan.need_scratch("stats", 4 * self.stats_rows * (2 * self.stats_ld + 1))
             plan.need_scratch("bwd", 4 * 2 * c * L.lib().yms_bn_bwd_rows(self.npix, c))
             plan.need_scratch("coef", 8 * c)
-            plan.need_scratch("wgrad", L.lib().yms_dwconv_wgrad_ws_bytes(self.sp))
+            # sized once here and passed as-is at backward time: the C side reads its tiling knobs
+            # on every call, so a recomputed size could outgrow the region reserved here
+            self.wg_ws = L.lib().yms_dwconv_wgrad_ws_bytes(self.sp)
+            plan.need_scratch("wgrad", self.wg_ws)
             self.cnt = plan.counter()
             if self.bnred is not None:
                 self.bnred.red_rows = L.lib().yms_dwconv_dgrad_rows(self.sp)
@@ -534,7 +538,7 @@ class DWConvOp(ConvOp):
             L.call("yms_dwconv_dgrad", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
-            wsz = L.lib().yms_dwconv_wgrad_ws_bytes(self.sp)
+            wsz = self.wg_ws
             if self.bnin is not None:
                 p = self.bnin
                 L.call("yms_dwconv_wgrad_bnin", self.sp, base + p.z, p.zld, 0, base + p.sc, base + p.sh, p.act, z,

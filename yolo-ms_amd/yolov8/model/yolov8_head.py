@@ -23,8 +23,13 @@ class Head(_YmsModule):
         self.num_classes = num_classes
         self.no = self.coordinates + num_classes
         self.stride = torch.zeros(3)
-        d, w, r = yolo_params(version)
-        in_c = [int(256 * w), int(512 * w), int(512 * w * r)]
+        if isinstance(version, str) and version.startswith("ms-"):
+            # YOLO-MS family (yolo_ms.py): the neck's calibrated widths, not yolo_params'
+            from yolov8.model.yolo_ms import ms_head_channels
+            in_c = list(ms_head_channels(version))
+        else:
+            d, w, r = yolo_params(version)
+            in_c = [int(256 * w), int(512 * w), int(512 * w * r)]
         co, nc = self.coordinates, num_classes
 
         def branch(cin, hid):

@@ -13,7 +13,7 @@ from torch import nn
 from yolov8.model.yolov8_backbone import Backbone
 from yolov8.model.yolov8_neck import Neck
 from yolov8.model.yolov8_head import Head
-from yolov8.model.yolo_ms import MSBackbone, MSNeck, is_ms_version, ms_params
+from yolov8.model.yolo_ms import MSBackbone, MSNeck, is_ms_version
 from yms import runner as _runner
 
 
@@ -25,7 +25,7 @@ class YOLOv8(nn.Module):
             # reference head (yolov8/model/yolo_ms.py; not in the reference's code)
             self.backbone = MSBackbone(version)
             self.neck = MSNeck(version)
-            self.head = Head(version=ms_params(version)[4], num_classes=num_classes, ch=dfl_ch)
+            self.head = Head(version=version, num_classes=num_classes, ch=dfl_ch)
             return
         self.backbone = Backbone(version)
         self.neck = Neck(version)
