@@ -32,8 +32,8 @@ import torch.nn.functional as F
 from oracle import model_ref as M
 
 # version -> ((c1, c2, c3, c4, c5), IB layers per branch)
-VERSIONS = {"ms-xs": ((24, 48, 96, 192, 192), 2),
-            "ms-s": ((40, 80, 128, 256, 256), 2),
+VERSIONS = {"ms-xs": ((24, 48, 112, 224, 192), 1),
+            "ms-s": ((32, 64, 160, 288, 288), 1),
             "ms-l": ((56, 112, 224, 448, 384), 2)}
 HKS = (3, 5, 7, 9)
 

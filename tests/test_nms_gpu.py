@@ -227,3 +227,51 @@ def test_nms_on_side_stream_overlapping_next_forward():
         for b in range(c0.numel()):
             n = int(c0[b])
             assert torch.equal(k0[b, :n], k1[b, :n]) and torch.equal(l0[b, :n], l1[b, :n])
+
+
+def _level_segments(B, seed, jitter=20.0, size=160.0):
+    """The bench's regime (random-init YOLOv8-s / YOLO-MS at 640): every anchor of a pyramid level
+    carries the same arg-max class, so each image has three segments of 6400 / 1600 / 400
+    candidates, with ~160-px boxes centred on the anchor grid."""
+    rng = np.random.default_rng(seed)
+    A, nc = 8400, 80
+    pred = np.zeros((B, A, 4 + nc), np.float32)
+    a0 = 0
+    for s, cls in ((8, 3), (16, 7), (32, 11)):
+        g = 640 // s
+        ys, xs = np.meshgrid(np.arange(g), np.arange(g), indexing="ij")
+        cx, cy = (xs.ravel() + 0.5) * s, (ys.ravel() + 0.5) * s
+        sl = slice(a0, a0 + g * g)
+        for b in range(B):
+            pred[b, sl, 0] = cx + rng.normal(0, 2, g * g)
+            pred[b, sl, 1] = cy + rng.normal(0, 2, g * g)
+            pred[b, sl, 2:4] = size + rng.uniform(-jitter, jitter, (g * g, 2))
+            pred[b, sl, 4:] = rng.uniform(0.0, 0.2, (g * g, nc))
+            pred[b, sl, 4 + cls] = rng.uniform(0.3, 0.7, g * g)
+        a0 += g * g
+    return pred
+
+
+@pytest.mark.parametrize("window", ["1", "0"])
+def test_window_and_kept_list_greedy_agree(monkeypatch, window):
+    """Big segments <= 8192 boxes take the window kernel by default (YMS_NMS_WINDOW=0: the kept-list
+    grid greedy): both are bit-exact against the oracle on the bench's level segments, on dense
+    single-class segments, at thresholds 0.45 / 0.5 / 0.6 / 0 / negative, and with NaN / inf /
+    zero-area boxes."""
+    monkeypatch.setenv("YMS_NMS_WINDOW", window)
+    for thr in (0.45, 0.5, 0.6):
+        assert _check(_level_segments(3, 21), 0.25, thr) > 0
+    rng = np.random.default_rng(23)
+    A = 8400
+    p = np.zeros((1, A, 5), np.float32)
+    p[..., :2] = rng.uniform(0, 640, (1, A, 2))
+    p[..., 2:4] = rng.uniform(5, 60, (1, A, 2))
+    p[..., 4] = rng.uniform(0.3, 1.0, (1, A))
+    assert _check(p, 0.25, 0.5) > 64
+    _check(p, 0.25, 0.0)
+    _check(p, 0.25, -0.25)
+    p[0, 1::97, 2] = 0.0
+    p[0, 5::61, 3] = np.nan
+    p[0, int(np.argmax(p[0, :, 4])), 2] = np.nan
+    p[0, 77, 1] = np.inf
+    _check(p, 0.25, 0.5)

@@ -38,7 +38,10 @@ def call(name, *args):
         sh = args[0].contents
         key = f"{sh.n}x{sh.h}x{sh.w} c{sh.c} k{sh.k}"
         fl = 2 * sh.n * sh.h * sh.w * sh.c * sh.k * sh.k
-    elif name.startswith(("yms_bn_act", "yms_affine")):
+    elif name == "yms_bn_act_bwd_finalize":       # (c, ws, rows, npix, ...)
+        key = f"npix {args[3]} c {args[0]}"
+        fl = 0
+    elif name.startswith(("yms_bn_act", "yms_affine")):   # (dtype, npix, c, ...)
         key = f"npix {args[1]} c {args[2]}"
         fl = 0
     else:

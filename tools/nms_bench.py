@@ -23,3 +23,10 @@ print("dense random-init-like (B=32, ~105/class): %.3f ms kept/img %s" % (timeit
 print("clustered (B=32, 20x30 boxes): %.3f ms" % timeit(clustered(B, nc))[0])
 one = dense[..., :5].copy(); one[..., 4] = rng.uniform(0, 1, (B, A))
 print("single class nc=1 (B=32, 8400 cand): %.3f ms" % timeit(one)[0])
+from test_nms_gpu import _level_segments
+lv = _level_segments(B, 5)
+for win in ("1", "0"):
+    os.environ["YMS_NMS_WINDOW"] = win
+    t, k = timeit(lv)
+    print("level segments 6400/1600/400 (B=32, bench regime) window=%s: %.3f ms kept/img %s" % (win, t, k[:4]))
+    os.environ["YMS_NMS_WINDOW"] = "1"

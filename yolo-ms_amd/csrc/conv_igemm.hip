@@ -40,7 +40,7 @@ struct NTParams {
   int OW;           // row-space width
   int stride, pad;
   int cpt;          // 16-B chunks per tap along source channels
-  uint32_t cpt_magic;   // kc / cpt == (kc * cpt_magic) >> 16 for every kc < nkt * 8 (host-checked)
+  uint64_t cpt_magic;   // kc / cpt == (kc * cpt_magic) >> 32 for every kc < nkt * 8 (host-checked)
   uint32_t src_bytes;   // byte extent of the source view's buffer (raw-buffer num_records, < 2^31)
   int Kc;           // valid K chunks
   int nkt;          // K tiles (4 chunks each)
@@ -564,7 +564,7 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
     } else {
       // per-lane K position: kc = kt*8 + q, tap = kc / cpt (exact multiply-shift, host-checked)
       const int kc = ld_kt * NT_KCH + q;
-      const int lt = (int)(((uint32_t)kc * p.cpt_magic) >> 16);
+      const int lt = (int)(((uint64_t)(uint32_t)kc * p.cpt_magic) >> 32);
       const int lc = kc - lt * p.cpt;
       int dy, dx;
       if (MODE == MODE_DGRAD2) {
@@ -1249,6 +1249,8 @@ static int nt_dgrad_mult() { static const int v = std::max(1, env_int("YMS_NT_DG
 struct NtpGeo { int bm, bn, occ; };
 static NtpGeo ntp_geo(int cfg) {
   const bool v6 = nt_variant() == 6;
+  if (cfg == 0 && nt_variant() == 7) return NtpGeo{256, 128, 1};
+  if (cfg == 0 && nt_variant() == 8) return NtpGeo{128, 128, 2};
   if (cfg == 0) return v6 ? NtpGeo{256, 128, 1} : NtpGeo{128, 128, 2};
   if (cfg == 1) return v6 ? NtpGeo{256, 64, 1} : NtpGeo{128, 64, 3};
   return NtpGeo{256, 32, 2};
@@ -1284,7 +1286,13 @@ static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st)
   p.tiles_n = cdiv(p.Ncols, g.bn);
   // 8-wave blocks at 2-3 per CU (4-6 waves per SIMD) hide the ds_read -> MFMA and barrier
   // latencies that 4-wave blocks expose
-  if (cfg == 0) {
+  if (cfg == 0 && nt_variant() == 7) {
+    // dev A/B: 256 x 128 tiles of 8 waves with 64 x 64 wave tiles (one LDS fragment read per MFMA)
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 2, 3, UNI, 1>, p, 256, gy, st, g.occ * mult, 512, stats);
+  } else if (cfg == 0 && nt_variant() == 8) {
+    // dev A/B: 128 x 128 tiles of 4 waves with 64 x 64 wave tiles
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 2, 2, UNI, 2>, p, 128, gy, st, g.occ * mult, 256, stats);
+  } else if (cfg == 0) {
     if (g.bm == 256)
       launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1>, p, 256, gy, st, g.occ * mult, 1024, stats);
     else
@@ -1330,9 +1338,9 @@ static bool set_src_geometry(NTParams& p, long n, long h, long w, long ld, int e
   const long bytes = n * h * w * ld * es;
   if (es == 2 && bytes >= (1l << 31) - (1l << 20)) return false;
   p.src_bytes = (uint32_t)std::min<long>(bytes, 0x7fffffffl);
-  p.cpt_magic = (65536u + (uint32_t)p.cpt - 1) / (uint32_t)p.cpt;
+  p.cpt_magic = ((1ull << 32) + (uint64_t)p.cpt - 1) / (uint64_t)p.cpt;
   for (int kc = 0; kc < max_kc; ++kc)
-    if ((int)(((uint32_t)kc * p.cpt_magic) >> 16) != kc / p.cpt) return false;
+    if ((int)(((uint64_t)(uint32_t)kc * p.cpt_magic) >> 32) != kc / p.cpt) return false;
   return true;
 }
 

@@ -606,6 +606,149 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
   }
 }
 
+// wgrad, k = 5 / 7 / 9, 16-bit types (default; YMS_DW_WG2=0 keeps the kernel above): the same lane
+// work as dwconv_wgrad_kernel -- lane (dy, ty, s) of a channel group keeps the K x 8 partial taps of
+// kernel row dy for its tile row and column segment in registers across all of the block's tiles --
+// on tiles shaped for the map and the kernel: TX = the forward's width (20 / 40 / 32: no idle
+// columns on the 20 / 40 / 80-wide maps) and TY rows such that K TY S of the 128 lanes of a group
+// are busy (the 8 x 32 tile kept 56-88 % of them busy and wasted 3/8 of its columns on 20-wide
+// maps), and with the NEXT tile's halo and dz chunks fetched into registers while the current tile
+// computes (the tile kernel staged each tile synchronously).  Same fixed-order reductions.
+template <int K, int TX>
+struct DwWg2 {
+  static constexpr int S = TX == 20 ? 1 : 2;
+  static constexpr int TY = TX == 20 ? (K == 5 ? 20 : 10) : (K == 5 ? 12 : (K == 7 ? 9 : 7));
+  static constexpr int SL = TX / S;
+  static constexpr int NA = K * TY * S;
+};
+
+template <typename T, int K, int TX>
+__global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad2_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
+                                                                  float* ws) {
+  using W = DwWg2<K, TX>;
+  constexpr int TY = W::TY, S = W::S, SL = W::SL, NA = W::NA;
+  static_assert(NA <= DW_WG_LPG && SL % 4 == 0 && sizeof(T) == 2, "dw wgrad2 lane mapping");
+  constexpr int HH = TY + K - 1, HW = TX + K - 1, P = K / 2;
+  constexpr int HRS = dw_rs(HW), DRS = dw_rs(TX);
+  constexpr int HALO_N = DW_G * HH * HW, DZ_N = DW_G * TY * TX;          // 16-B items per tile
+  constexpr int ITEMS = (HALO_N + DZ_N + DW_WG_NT - 1) / DW_WG_NT;
+  constexpr int HALO = DW_G * HH * HRS, DZL = DW_G * TY * DRS;
+  constexpr int STAGE_B = (HALO + DZL) * (int)sizeof(Raw8<T>);
+  constexpr int RED_B = NA * K * 8 * (int)sizeof(float);
+  __shared__ __attribute__((aligned(16))) char smem[STAGE_B > RED_B ? STAGE_B : RED_B];
+  Raw8<T>* halo = reinterpret_cast<Raw8<T>*>(smem);
+  Raw8<T>* dzl = halo + HALO;
+  float* red = reinterpret_cast<float*>(smem);
+  const int c0 = blockIdx.y * DW_CB;
+  const int tid = threadIdx.x;
+  const int g = tid / DW_WG_LPG, l = tid % DW_WG_LPG;
+  const bool active = l < NA;
+  const int ll = active ? l : 0;
+  const int dy = ll / (TY * S), r = ll % (TY * S);
+  const int ty = r / S, sx = (r % S) * SL;
+  const int tiles_x = (p.W + TX - 1) / TX, tiles_y = (p.H + TY - 1) / TY;
+  const int per_img = tiles_x * tiles_y, ntiles = p.N * per_img;
+  const T* src = reinterpret_cast<const T*>(p.src);
+  const T* dzp = reinterpret_cast<const T*>(dz);
+  // item it of a tile: halo chunk (g, hy, hx) for it < HALO_N, else dz chunk (g, ty, tx)
+  auto fetch = [&](int tile, Raw8<T> (&buf)[ITEMS]) {
+    const int n = tile / per_img, rem = tile - n * per_img;
+    const int y0 = (rem / tiles_x) * TY, x0 = (rem % tiles_x) * TX;
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int it = tid + j * DW_WG_NT;
+#pragma unroll
+      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) buf[j].v[k] = u32x4{0u, 0u, 0u, 0u};
+      int y, x, c;
+      const T* base;
+      long ld, off;
+      if (it < HALO_N) {
+        const int gg = it / (HH * HW), rr = it - gg * (HH * HW);
+        y = y0 + rr / HW - P; x = x0 + rr % HW - P; c = c0 + 8 * gg;
+        base = src; ld = p.src_ld; off = p.src_off;
+      } else if (it < HALO_N + DZ_N) {
+        const int i2 = it - HALO_N, gg = i2 / (TY * TX), rr = i2 - gg * (TY * TX);
+        y = y0 + rr / TX; x = x0 + rr % TX; c = c0 + 8 * gg;
+        base = dzp; ld = dz_ld; off = dz_off;
+      } else {
+        continue;
+      }
+      if (y >= 0 && y < p.H && x >= 0 && x < p.W && c < p.C)
+        load_raw8(base + (((long)n * p.H + y) * p.W + x) * ld + off + c, min(8, p.C - c), buf[j]);
+    }
+  };
+  auto store = [&](const Raw8<T> (&buf)[ITEMS]) {
+#pragma unroll
+    for (int j = 0; j < ITEMS; ++j) {
+      const int it = tid + j * DW_WG_NT;
+      if (it < HALO_N) {
+        const int gg = it / (HH * HW), rr = it - gg * (HH * HW);
+        halo[(gg * HH + rr / HW) * HRS + rr % HW] = buf[j];
+      } else if (it < HALO_N + DZ_N) {
+        const int i2 = it - HALO_N, gg = i2 / (TY * TX), rr = i2 - gg * (TY * TX);
+        dzl[(gg * TY + rr / TX) * DRS + rr % TX] = buf[j];
+      }
+    }
+  };
+  float part[K][8];
+#pragma unroll
+  for (int dx = 0; dx < K; ++dx)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) part[dx][k] = 0.0f;
+  Raw8<T> buf[ITEMS];
+  if ((int)blockIdx.x < ntiles) fetch(blockIdx.x, buf);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+    __syncthreads();      // the previous tile's LDS reads are done
+    store(buf);
+    __syncthreads();
+    if (tile + (int)gridDim.x < ntiles) fetch(tile + gridDim.x, buf);   // in flight during the FMAs
+    if (active) {
+      const Raw8<T>* hrow = halo + (g * HH + ty + dy) * HRS + sx;
+      const Raw8<T>* drow = dzl + (g * TY + ty) * DRS + sx;
+#pragma unroll 1
+      for (int x4 = 0; x4 < SL; x4 += 4) {
+        float d[4][8];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) unpack8(drow[x4 + i], d[i]);
+#pragma unroll
+        for (int q = 0; q < 4 + K - 1; ++q) {
+          float v[8];
+          unpack8(hrow[x4 + q], v);
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const int dx = q - i;
+            if (dx >= 0 && dx < K) {
+#pragma unroll
+              for (int k = 0; k < 8; ++k) part[dx][k] += v[k] * d[i][k];
+            }
+          }
+        }
+      }
+    }
+  }
+  // fixed-order reduction over the (ty, s) lanes of each kernel row, one channel group at a time
+  for (int gg = 0; gg < DW_G; ++gg) {
+    __syncthreads();
+    if (g == gg && active) {
+      float* rp = red + l * K * 8;
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) {
+        *reinterpret_cast<f32x4*>(rp + dx * 8) = f32x4{part[dx][0], part[dx][1], part[dx][2], part[dx][3]};
+        *reinterpret_cast<f32x4*>(rp + dx * 8 + 4) = f32x4{part[dx][4], part[dx][5], part[dx][6], part[dx][7]};
+      }
+    }
+    __syncthreads();
+    for (int it = tid; it < K * K * 8; it += DW_WG_NT) {
+      const int t = it / 8, k = it - t * 8;
+      const int ddy = t / K, ddx = t - ddy * K;
+      float s = 0.f;
+      for (int rr = 0; rr < TY * S; ++rr) s += red[((ddy * TY * S + rr) * K + ddx) * 8 + k];
+      const int cc = c0 + 8 * gg + k;
+      if (cc < p.C) ws[((long)blockIdx.x * K * K + t) * p.C + cc] = s;
+    }
+  }
+}
+
 // wgrad, k = 3: the forward's strip walker (TY x TX tiles, RX = 4 pixels per lane, the input rows
 // in an LDS-DMA ring, the next tile's rows and dz chunks in flight while the current tile
 // computes).  Every lane keeps the 3 x 3 x 8 partial taps of its pixels in registers across the
@@ -1020,6 +1163,20 @@ static dim3 dw_wgk_grid(const yms_dw_shape* s, DwParams& p) {
   return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
 }
 
+static bool dw_wg2(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32 && dw_env("YMS_DW_WG2", 1) != 0; }
+static void dw_wg2_tile(const yms_dw_shape* s, int& tx, int& ty) {
+  tx = dw_fwd_tx(s);    // DwWg2<K, TX>::TY
+  ty = tx == 20 ? (s->k == 5 ? 20 : 10) : (s->k == 5 ? 12 : (s->k == 7 ? 9 : 7));
+}
+// dwconv_wgrad2_kernel grid: tiles of one channel group per block, about two blocks per CU in total
+static int dw_wg2_blocks(const yms_dw_shape* s) {
+  int tx, ty;
+  dw_wg2_tile(s, tx, ty);
+  const long tiles = (long)s->n * ((s->w + tx - 1) / tx) * ((s->h + ty - 1) / ty);
+  const int cg = (s->c + DW_CB - 1) / DW_CB;
+  return (int)std::max(1l, std::min(tiles, std::max(1l, (long)(2 * conv_cu_count()) / cg)));
+}
+
 // spatial partitions of the wgrad grid: about 1024 blocks in total over the channel groups (two
 // 512-thread blocks fit a CU), each walking several tiles so the ws rows stay few
 static int dw_wgrad_blocks(const yms_dw_shape* s) {
@@ -1286,7 +1443,8 @@ size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s) {
     DwParams p{};
     return (size_t)dw_wg3_grid(s, p).x * s->k * s->k * s->c * sizeof(float);
   }
-  const size_t tile = (size_t)dw_wgrad_blocks(s) * s->k * s->k * s->c * sizeof(float);
+  size_t tile = (size_t)dw_wgrad_blocks(s) * s->k * s->k * s->c * sizeof(float);
+  if (dw_wg2(s)) tile = std::max(tile, (size_t)dw_wg2_blocks(s) * s->k * s->k * s->c * sizeof(float));
   if (dw_wgk(s)) {
     // the input-affine (BNIN) weight gradient keeps the tile kernel: size for both
     DwParams p{};
@@ -1346,6 +1504,26 @@ static yms_status dw_wgrad_impl(const yms_dw_shape* s, const void* x, int x_ld, 
     const int KK2 = s->k * s->k;
     hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
                        (int)grid.x, s->c, KK2, dw, accumulate);
+    return launch_status();
+  }
+  if (dw_wg2(s) && !bnin) {
+    const int blocks = dw_wg2_blocks(s);
+    const dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
+    hipStream_t st = (hipStream_t)stream;
+    const int TX = dw_fwd_tx(s);
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
+      if (s->k == 5) hipLaunchKernelGGL((dwconv_wgrad2_kernel<TT, 5, TXX>), grid, dim3(DW_WG_NT), 0, st, p,
+                                        (const char*)dz, dz_ld, dz_off, ws);
+      else if (s->k == 7) hipLaunchKernelGGL((dwconv_wgrad2_kernel<TT, 7, TXX>), grid, dim3(DW_WG_NT), 0, st, p,
+                                             (const char*)dz, dz_ld, dz_off, ws);
+      else hipLaunchKernelGGL((dwconv_wgrad2_kernel<TT, 9, TXX>), grid, dim3(DW_WG_NT), 0, st, p, (const char*)dz,
+                              dz_ld, dz_off, ws);
+    }));
+    yms_status e = launch_status();
+    if (e != YMS_OK) return e;
+    const int KK2 = s->k * s->k;
+    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
+                       blocks, s->c, KK2, dw, accumulate);
     return launch_status();
   }
   dw_tiles(s, p.tiles_x, p.tiles_y);

@@ -223,8 +223,14 @@ bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
   // register-staged kernel (its 32-row / 64-column tiles) unless YMS_WG_RING=2
   q.bm = s->cout <= 64 ? 64 : 128;
   q.bn = kf <= 64 ? 64 : 128;
-  if (q.bm == 64 && q.bn == 64) return false;
-  if (on != 2 && s->cout <= 32) return false;
+  // YMS_WG_RING_SMALL=1 (dev A/B): the 64 x 64 GEMMs (and <= 32 output channels) on a 64 x 128 ring
+  // tile, the unused columns zero-filled by the range check (no bytes fetched for them)
+  const int small = env_int_wr("YMS_WG_RING_SMALL", 0);   // per call: dev tools switch it
+  if (q.bm == 64 && q.bn == 64) {
+    if (!small) return false;
+    q.bn = 128;
+  }
+  if (on != 2 && !small && s->cout <= 32) return false;
   const int var = env_int_wr("YMS_WG_RING_VAR", 0);
   q.var = ((var == 1 || var == 3) && !(q.bm == 128 && q.bn == 128)) ? 0 : var;
   q.kp = (q.var == 1 || q.var == 3) ? 32 : 64;

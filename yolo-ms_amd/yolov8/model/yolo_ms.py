@@ -29,8 +29,10 @@ build's own CPU restatement oracle/ms_ref.py, NOT reference-pinned):
 
 Sizes (``MS_ARCH``): the stage widths and the IB depth are calibrated so that parameters and
 forward multiply-accumulates at 640x640 match the model-zoo table (its "FLOPs" are MACs, the
-mmengine / fvcore convention; see ``ms_complexity`` and tests/test_ms_cpu.py).  All three sizes use
-two IB layers per branch.  The reference's ``yolo_params`` keeps raising ValueError for every
+mmengine / fvcore convention; see ``ms_complexity`` and tests/test_ms_cpu.py).  IB layers per
+branch: one for XS / S, two for YOLO-MS (the paper's three-layer depth scaled by 1/3 and 2/3);
+among the width tables that land within 2% of both figures, the one with the fewest activation
+elements was taken (the training step is bound by the BN passes over them).  The reference's ``yolo_params`` keeps raising ValueError for every
 string outside 'n'..'x', 'ms-*' included.
 """
 from torch import nn
@@ -39,8 +41,8 @@ from yolov8.model.components import Conv, SPPF, Upsample, _YmsModule
 
 # version -> ((stem c1, stage widths c2 (stride 4), c3 (P3), c4 (P4), c5 (P5)), IB layers per branch)
 MS_ARCH = {
-    "ms-xs": ((24, 48, 96, 192, 192), 2),
-    "ms-s": ((40, 80, 128, 256, 256), 2),
+    "ms-xs": ((24, 48, 112, 224, 192), 1),
+    "ms-s": ((32, 64, 160, 288, 288), 1),
     "ms-l": ((56, 112, 224, 448, 384), 2),
 }
 # model_zoos.md:21-53 (params in M, FLOPs = MACs in G at 640x640) of the upstream YOLO-MS family
