@@ -212,7 +212,8 @@ __device__ __forceinline__ Raw8<T> pack_raw8(const float (&v)[8]) {
 }
 
 template <typename T, int K, int MODE, int TX = DW_TX, int G = DW_G>
-__global__ __launch_bounds__(G * 64, (MODE == 3 ? (G == 8 ? 1 : 2) : (G == 8 ? 2 : DwOcc<T, K>::v)))
+__global__ __launch_bounds__(G * 64, (MODE == 3 ? (G == 8 ? 1 : (sizeof(T) == 4 && K > 3 ? 1 : 2))
+                                                 : (G == 8 ? 2 : DwOcc<T, K>::v)))
 void dwconv_kernel(DwParams p) {
   constexpr int CB = G * 8, NT = G * 64;
   constexpr int TY = DwTy<TX>::v, CGX = TX / DW_RX;

@@ -761,7 +761,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
 }
 
 // Greedy suppression of a sorted big segment of at most NMS_WIN_MAX boxes, by WINDOWS of kept-box
-// candidates (default; YMS_NMS_WINDOW=0 keeps nms_big_greedy_kernel for every big segment).  The
+// candidates (opt-in, YMS_NMS_WINDOW=1; nms_big_greedy_kernel is the default, see the dispatch).  The
 // block stages the segment's boxes in LDS with an alive bit per box and repeats:
 //   1. wave 0 takes the next (up to) 64 alive candidates in score order (the window),
 //   2. resolves them serially among themselves (a candidate survives unless a kept window member
@@ -1044,10 +1044,12 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
       const char* e = getenv("YMS_NMS_GRID_MIN_KEPT");
       return e ? atoi(e) : 128;
     }();
-    // segments of at most NMS_WIN_MAX boxes: the window kernel (YMS_NMS_WINDOW=0: all on the
-    // kept-list greedy, dev A/B; read per call)
+    // YMS_NMS_WINDOW=1: segments of at most NMS_WIN_MAX boxes on the window kernel (opt-in, read
+    // per call).  Measured (profiles/r04c_nms_kernels.txt): 267 vs 343 us on the bench's level
+    // segments (~115 kept of 6400), but 4.0 ms on uniform small boxes where most candidates are kept
+    // (its test phase is candidates x kept boxes on one CU; the grid greedy prunes spatially).
     const char* wenv = getenv("YMS_NMS_WINDOW");
-    const int win_max = (wenv && atoi(wenv) == 0) ? 0 : NMS_WIN_MAX;
+    const int win_max = (wenv && atoi(wenv) == 1) ? NMS_WIN_MAX : 0;
     if (win_max > 0)
       hipLaunchKernelGGL(nms_window_kernel, dim3(segs), dim3(1024), NMS_WIN_LDS, st, A, nc, thr_f, full, w);
     if (A > win_max)

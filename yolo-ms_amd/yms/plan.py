@@ -126,6 +126,25 @@ class GradTracker:
         if not self._covered(v):
             self._zero_buf(v)
 
+    def release(self, v):
+        """The producer of v has taken its gradient (backward order): the slice's gradient is dead,
+        so a later (earlier-in-forward) writer of the same memory stores instead of accumulating.
+        Only matters where one buffer slice holds two tensors in turn (MSBlock: Y_{i+1} written over
+        X_{i+1}); buffers with zeroed padding always accumulate and are never reused that way."""
+        if v.buf.zero:
+            return
+        lo, hi = self._iv(v)
+        out = []
+        for a, b in self.written.get(v.buf.idx, []):
+            if b <= lo or a >= hi:
+                out.append((a, b))
+                continue
+            if a < lo:
+                out.append((a, lo))
+            if b > hi:
+                out.append((hi, b))
+        self.written[v.buf.idx] = out
+
     def write(self, v):
         """-> accumulate flag (0 = first writer, plain store)."""
         if v.buf.zero:                       # padded channels must stay zero: zero whole buffer
@@ -207,6 +226,8 @@ class ConvOp:
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
         self.red_rows = 0        # > 0: its BN-backward partial rows come from its consumer's dgrad
         self.bnin_by = None      # depthwise consumer that forms act(BN(z)) itself (no affine pass)
+        self.pro_by = None       # consumer conv that forms (and stores) this op's x = act(BN(z))
+        self.pro = None          # producer whose act(BN(z)) this conv forms in its prologue
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -281,6 +302,11 @@ class ConvOp:
         if stem:
             L.call("yms_conv_stem_fwd", self.sp, rt.stem_x[self.stem_input].data_ptr(), m.conv.weight.data_ptr(),
                    base + self.z, self.zld, 0, None, None, L.ACT_NONE, stats, self.stats_ld, rt.st)
+        elif self.pro is not None:
+            # the producer's affine pass is folded in: read its z, form x in the prologue and store it
+            q = self.pro
+            L.call("yms_conv_fwd_pro", self.sp, base + q.z, q.zld, 0, base + q.sc, base + q.sh, q.act, rt.a(x), xl,
+                   x.off, base + self.t_wp, base + self.z, self.zld, 0, stats, rt.st)
         else:
             L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
                    None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
@@ -289,7 +315,7 @@ class ConvOp:
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
-        if self.bnin_by is None:
+        if self.bnin_by is None and self.pro_by is None:
             L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
                    base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
 
@@ -456,6 +482,7 @@ class DWConvOp(ConvOp):
         self.dw_flops = 2 * self.npix * c * k * k
         self.bnred = None       # producer ConvOp whose BN-backward reduce is fused into this dgrad
         self.bnin = None        # producer ConvOp whose act(BN(z)) this op forms from z (fwd, wgrad)
+        self.pro_by = None      # consumer conv that forms (and stores) this op's output in its prologue
 
     def layout(self, plan, La, Le):
         es, c = plan.es, self.c
@@ -512,8 +539,9 @@ class DWConvOp(ConvOp):
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
-        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
-               base + self.sh, self.act, None, 0, 0, rt.a(y), y.buf.ld, y.off, rt.st)
+        if self.pro_by is None:
+            L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+                   base + self.sh, self.act, None, 0, 0, rt.a(y), y.buf.ld, y.off, rt.st)
 
     def bwd(self, rt):
         x, y = self.x, self.y
@@ -723,6 +751,7 @@ class Plan:
         self.n_counters = 0
         self.stem_inputs = self._find_stems()
         self._find_dw_bnred()
+        self._find_pro()
         La, Le = Layout(), Layout()
         for buf in self.bufs:
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
@@ -746,6 +775,9 @@ class Plan:
             self.seed_acc = [T.write(v) for v in self.outputs]
             for op in reversed(self.ops):
                 op.plan_grads(T)
+                y = getattr(op, "y", None)
+                if isinstance(y, View) and not any(y is o for o in self.outputs):
+                    T.release(y)
             for op in self.ops:
                 if getattr(op, "bnred", None) is not None and op.acc_x:
                     # the fused dgrad stores: keep the separate reduce if dx must accumulate
@@ -822,6 +854,52 @@ class Plan:
             if bnin:
                 d.bnin = p
                 p.bnin_by = d
+
+    def _find_pro(self):
+        """Training, 16-bit: a Conv op whose input view is exactly the output of one earlier Conv /
+        depthwise op (no residual in that op's affine pass) and which is the FIRST reader of it
+        takes the producer's BN + activation as an A-operand prologue (yms_conv_fwd_pro): it reads
+        the producer's z, forms x = act(z * scale + shift) in LDS and stores x from its centre-tap
+        tiles, so the producer's affine pass goes (its write stays, its read of z is the conv's own
+        input read).  x is still materialised, so every later reader and the whole backward are
+        unchanged.  Stride-1 'same' consumers only (their centre tap covers every input pixel once).
+        YMS_PRO=0 keeps the separate affine passes."""
+        if not self.training or self.dt == L.F32 or os.environ.get("YMS_PRO", "1") == "0":
+            return
+        for i, c in enumerate(self.ops):
+            if type(c) is not ConvOp or c.stem_input is not None:
+                continue
+            if not L.lib().yms_conv_fwd_pro_supported(c.sp):
+                continue
+            # 3x3 consumers transform every input element once per tap (im2col A tiles): measured
+            # slower than the affine pass they replace (YOLOv8-s 18.8 -> 20.5 ms/step with them,
+            # profiles/r04c_pro_ab.txt); YMS_PRO=3 includes them (dev A/B)
+            if c.shape.k != 1 and os.environ.get("YMS_PRO", "1") != "3":
+                continue
+            x = c.x
+            prod = None
+            for j in range(i - 1, -1, -1):
+                q = self.ops[j]
+                y = getattr(q, "y", None)
+                if isinstance(y, View) and y.buf is x.buf and not (y.off + y.c <= x.off or x.off + x.c <= y.off):
+                    prod = (j, q)
+                    break
+            if prod is None:
+                continue
+            j, q = prod
+            if type(q) not in (ConvOp, DWConvOp) or q.y.off != x.off or q.y.c != x.c or q.res is not None:
+                continue
+            if getattr(q, "bnin_by", None) is not None or q.pro_by is not None or q.act not in (L.ACT_NONE, L.ACT_SILU):
+                continue
+            if getattr(q, "stem_input", None) is not None:
+                continue
+            # no op between producer and consumer reads the producer's output
+            between = self.ops[j + 1:i]
+            if any(isinstance(a, View) and a.buf is x.buf and not (a.off + a.c <= x.off or x.off + x.c <= a.off)
+                   for op in between for k, a in vars(op).items() if k != "y"):
+                continue
+            q.pro_by = c
+            c.pro = q
 
     def counter(self):
         """Reserve one 16-B arrival counter in the grad scratch (-> its index)."""

@@ -109,16 +109,17 @@ class MSBlock(_YmsModule):
 
     def emit(self, b, x, out=None):
         mid = self.mid
+        # one buffer holds [X_1 | X_2 | X_3] and becomes the concat [Y_1 | Y_2 | Y_3] in place:
+        # Y_1 = X_1 needs no copy, and Y_{i+1} is written over X_{i+1} once X_{i+1} + Y_i has been
+        # formed (the gradient tracker releases a slice when its producer's backward has taken it)
         t = self.in_conv.emit(b, x)                           # [X_1 | X_2 | X_3]
-        cat = b.new(t.h, t.w, 3 * mid, name="ms_cat")         # [Y_1 | Y_2 | Y_3]
-        b.add(t.slot(0, mid), None, out=cat.slot(0, mid))     # Y_1 = X_1
-        prev = cat.slot(0, mid)
+        prev = t.slot(0, mid)                                 # Y_1 = X_1
         for i, br in enumerate(self.branches):
             s = b.add(t.slot((i + 1) * mid, mid), prev)       # X_{i+1} + Y_i
             for j, layer in enumerate(br):
-                s = layer.emit(b, s, out=cat.slot((i + 1) * mid, mid) if j == len(br) - 1 else None)
+                s = layer.emit(b, s, out=t.slot((i + 1) * mid, mid) if j == len(br) - 1 else None)
             prev = s
-        return self.out_conv.emit(b, cat, out=out)
+        return self.out_conv.emit(b, t, out=out)             # [Y_1 | Y_2 | Y_3]
 
     def forward(self, x):
         return self._yms_run(x)[0]
