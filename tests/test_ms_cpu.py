@@ -73,3 +73,37 @@ def test_sizes_match_model_zoo_table(v):
     assert abs(macs / tm - 1) < 0.02, macs
     # with fvcore's one op per batch-norm / upsample output element the total stays within 3%
     assert abs((macs + elems) / tm - 1) < 0.03, macs + elems
+
+
+def test_msblock_concat_aliases_input_conv_output():
+    """[X_1 | X_2 | X_3] becomes [Y_1 | Y_2 | Y_3] in place: no Y_1 = X_1 copy, the IB outputs are
+    written over X_2 / X_3 after the branch sums read them, out_conv reads the in_conv's buffer;
+    the gradient tracker stores (not accumulates) dX_{i+1} over the consumed dY_{i+1}."""
+    from yms.plan import AddOp, ConvOp
+    m = YOLOv8("ms-s", 80).train()
+    p = runner.get_plan(m, [torch.empty(2, 3, 128, 128, device="meta")], torch.bfloat16, True)
+    blk = m.backbone.ms_4
+    ops = {id(getattr(op, "mod", None)): op for op in p.ops if isinstance(op, ConvOp)}
+    cin, cout = ops[id(blk.in_conv)], ops[id(blk.out_conv)]
+    assert cout.x.buf is cin.y.buf and cout.x.off == cin.y.off and cout.x.c == cin.y.c
+    adds = [op for op in p.ops if isinstance(op, AddOp) and op.a.buf is cin.y.buf]
+    assert len(adds) == 2 and all(op.b is not None for op in adds)          # X_2 + Y_1, X_3 + Y_2 only
+    last = [ops[id(br[-1].out_conv)] for br in blk.branches]
+    mid = blk.mid
+    assert [(v.y.buf is cin.y.buf, v.y.off) for v in last] == [(True, mid), (True, 2 * mid)]
+    # backward: each branch-sum backward stores dX_{i+1} (the slice's dY_{i+1} was taken by the IB)
+    assert [op.acc[0] for op in adds] == [0, 0]
+    # ... and accumulates dY_i into the slice out_conv's dgrad stored
+    assert [op.acc[1] for op in adds] == [1, 1]
+
+
+def test_grad_tracker_release():
+    from yms.plan import Buf, GradTracker, View
+    b = Buf(0, 1, 4, 4, 24, "t", False)
+    T = GradTracker()
+    whole, s1 = View(b, 0, 24), View(b, 8, 8)
+    assert T.write(whole) == 0          # out_conv dgrad: [dY1|dY2|dY3]
+    T.read(s1)                          # the IB's backward takes dY2 ...
+    T.release(s1)                       # ... and the slice is dead
+    assert T.write(s1) == 0             # dX2 stored
+    assert T.write(View(b, 0, 8)) == 1  # dY1 += ...

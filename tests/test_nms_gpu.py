@@ -12,6 +12,22 @@ from yms import ops
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(params=["default", "graph", "nograph"], autouse=True)
+def nms_route(request, monkeypatch):
+    """Every case runs three ways: the default routing (graph kernels for segments of >= 2048 finite
+    boxes whose expected candidates per box are <= 256, the dense rest to the big-segment kernels),
+    the graph kernels on every segment of >= 128 finite boxes (YMS_NMS_GRAPH_MIN=128,
+    YMS_NMS_GRAPH_MAXC=0), and without them (YMS_NMS_GRAPH_MIN=0: class / big-segment kernels)."""
+    monkeypatch.delenv("YMS_NMS_GRAPH_MIN", raising=False)
+    monkeypatch.delenv("YMS_NMS_GRAPH_MAXC", raising=False)
+    if request.param == "graph":
+        monkeypatch.setenv("YMS_NMS_GRAPH_MIN", "128")
+        monkeypatch.setenv("YMS_NMS_GRAPH_MAXC", "0")
+    elif request.param == "nograph":
+        monkeypatch.setenv("YMS_NMS_GRAPH_MIN", "0")
+    return request.param
+
+
 def clustered(B, nc, K=20, J=30, A=8400, seed=0):
     """SURVEY 8d input set 2: K objects x J jittered boxes, Beta(2,5) scores, uniform labels."""
     rng = np.random.default_rng(seed)
@@ -275,3 +291,60 @@ def test_window_and_kept_list_greedy_agree(monkeypatch, window):
     p[0, int(np.argmax(p[0, :, 4])), 2] = np.nan
     p[0, 77, 1] = np.inf
     _check(p, 0.25, 0.5)
+
+
+def _single(b, s, thr):
+    ref = onms.nms(b, s, thr)
+    got = ops.nms(torch.from_numpy(b).cuda(), torch.from_numpy(s).cuda(), thr).cpu().numpy()
+    assert np.array_equal(got, ref), (thr, len(got), len(ref))
+    return len(ref)
+
+
+def test_graph_nms_edge_cases(monkeypatch, nms_route):
+    """The graph kernels on every segment of >= 32 boxes (YMS_NMS_GRAPH_MIN=32): suppressee lists
+    beyond their 254-entry capacity (identical boxes: the full-rectangle rescan), long suppression
+    chains (one decision round per link), mixed tiny / huge boxes (search rectangles spanning the
+    grid), degenerate boxes mixed in, all centres equal, thresholds 0 / 0.999 / 1, exact ties."""
+    if nms_route == "nograph":
+        pytest.skip("graph kernels forced on below")
+    monkeypatch.setenv("YMS_NMS_GRAPH_MIN", "32")
+    # "graph": every segment on the graph kernels; "default": dense ones (the identical boxes, the
+    # clusters) routed by the build kernel to the big-segment kernels, down to 32 boxes
+    monkeypatch.setenv("YMS_NMS_GRAPH_MAXC", "0" if nms_route == "graph" else "256")
+    rng = np.random.default_rng(31)
+    # identical boxes, distinct and tied scores
+    b = np.tile(np.array([[10, 20, 50, 70]], np.float32), (2000, 1))
+    s = rng.uniform(0, 1, 2000).astype(np.float32)
+    s[::7] = 0.5
+    assert _single(b, s, 0.5) == 1
+    # a chain: box k overlaps k-1 and k+1 only (IoU 0.54; k+-2: 0.25), scores decreasing along the chain
+    n = 700
+    x = np.arange(n, dtype=np.float32) * 3.0
+    b = np.stack([x, np.zeros(n, np.float32), x + 10.0, np.full(n, 10.0, np.float32)], 1)
+    s = np.linspace(1.0, 0.1, n).astype(np.float32)
+    assert _single(b, s, 0.5) == n // 2
+    _single(b, s[::-1].copy(), 0.5)
+    # mixed scales, degenerate boxes, equal centres
+    for trial in range(6):
+        n = int(rng.integers(40, 3000))
+        c = rng.uniform(0, 640, (n, 2))
+        wh = np.exp(rng.uniform(-3, 6, (n, 2)))
+        if trial == 1:
+            c[:] = c[0]
+        b = np.concatenate([c - wh / 2, c + wh / 2], 1).astype(np.float32)
+        if trial == 2:
+            b[::13, 2] = b[::13, 0]                 # zero width
+            b[1::17, 3] = b[1::17, 1] - 1.0         # inverted
+        s = rng.uniform(0, 1, n).astype(np.float32)
+        s[::11] = 0.25
+        for thr in (0.0, 0.3, 0.45, 0.5, 0.7, 0.999, 1.0):
+            _single(b, s, thr)
+    # class-wise: clustered detections with every class segment >= 32 on the graph kernels
+    for iou in (0.45, 0.6):
+        assert _check(clustered(3, 4, K=30, J=40, seed=4), 0.25, iou) > 0
+    # exact-threshold pairs inside a larger segment
+    base = np.array([[0, 0, 10, 10], [0, 0, 10, 5], [0, 0, 10, 7.5]], np.float32)
+    b = np.concatenate([base + 20 * k for k in range(100)], 0)
+    s = np.tile(np.array([0.9, 0.8, 0.7], np.float32), 100)
+    for thr in (0.45, 0.5, 0.6, 0.75):
+        _single(b, s, thr)

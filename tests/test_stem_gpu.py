@@ -26,7 +26,7 @@ def _ref(x, w, dt):
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("n,h,w,cin,cout", [(2, 64, 64, 3, 32), (3, 37, 70, 3, 48), (1, 130, 66, 2, 16),
-                                            (2, 40, 40, 1, 80), (1, 17, 9, 3, 96)])
+                                            (2, 40, 40, 1, 80), (1, 17, 9, 3, 96), (2, 48, 64, 3, 24)])
 def test_stem_eval_affine_silu(dt, n, h, w, cin, cout):
     g = torch.Generator().manual_seed(n * 1000 + h + cout)
     x = torch.randn(n, cin, h, w, generator=g) * 2.0
@@ -51,7 +51,7 @@ def test_stem_eval_affine_silu(dt, n, h, w, cin, cout):
     assert err <= tol * max(1.0, ref.abs().max().item()), err
 
 
-@pytest.mark.parametrize("n,h,w,cout", [(2, 64, 64, 32), (3, 45, 77, 48)])
+@pytest.mark.parametrize("n,h,w,cout", [(2, 64, 64, 32), (3, 45, 77, 48), (2, 48, 64, 24), (2, 40, 40, 56)])
 def test_stem_training_z_and_statistics(n, h, w, cout):
     dt = "bf16"
     g = torch.Generator().manual_seed(h * w + cout)
@@ -106,13 +106,21 @@ def test_model_stem_path_matches_generic_path(v, training, monkeypatch):
     from yms import set_compute_dtype
     from yolov8.yolov8 import YOLOv8
 
+    from oracle import model_ref as M
+    from oracle import ms_ref
+
+    # the well-conditioned fixture: at the default random init the graphs are chaotic enough
+    # (ms-xs bf16 output drift ~0.4 on the CPU alone) that the stem's fp32 statistics summation
+    # order (1e-7 relative in the batch mean) flips a few bf16 roundings and grows to 0.2 at the head
+    sd = M.ordered_init((ms_ref if v.startswith("ms") else M).init_params(v, 80))
     torch.manual_seed(0)
     x = torch.randn(2, 3, 96, 128, device="cuda")
     outs = {}
     for stem in ("1", "0"):
         monkeypatch.setenv("YMS_STEM", stem)
-        torch.manual_seed(1)
-        m = YOLOv8(v, 80).cuda()
+        m = YOLOv8(v, 80)
+        m.load_state_dict(sd)
+        m = m.cuda()
         set_compute_dtype(m, torch.bfloat16)
         m.train(training)
         if not training:
@@ -130,7 +138,8 @@ def test_model_stem_path_matches_generic_path(v, training, monkeypatch):
 
 
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
-@pytest.mark.parametrize("n,h,w,cout", [(2, 64, 64, 32), (3, 45, 78, 48), (1, 33, 20, 16)])
+@pytest.mark.parametrize("n,h,w,cout", [(2, 64, 64, 32), (3, 45, 78, 48), (1, 33, 20, 16), (2, 48, 64, 24),
+                                       (2, 40, 40, 56)])
 def test_stem_wgrad_with_fused_bn_backward(dt, n, h, w, cout):
     """yms_conv_stem_wgrad = BN+SiLU backward apply (bn_bwd_apply_kernel's dz, rounded to the
     dtype) followed by the conv weight gradient against the NCHW input, vs fp64 torch."""
