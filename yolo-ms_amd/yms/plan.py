@@ -863,8 +863,11 @@ class Plan:
         tiles, so the producer's affine pass goes (its write stays, its read of z is the conv's own
         input read).  x is still materialised, so every later reader and the whole backward are
         unchanged.  Stride-1 'same' consumers only (their centre tap covers every input pixel once).
-        YMS_PRO=0 keeps the separate affine passes."""
-        if not self.training or self.dt == L.F32 or os.environ.get("YMS_PRO", "1") == "0":
+        Opt-in (YMS_PRO=1: 1x1 consumers; YMS_PRO=3: also 3x3): the bytes it removes (the affine
+        pass's z read) do not pay for the prologue conv's lower occupancy -- interleaved on one box,
+        YOLOv8-s 18.36 vs 18.38 ms/step and YOLO-MS-S 35.83 vs 36.75 ms/step, off vs 1x1 on
+        (profiles/r04q_pro_1x1_ab.txt)."""
+        if not self.training or self.dt == L.F32 or os.environ.get("YMS_PRO", "0") == "0":
             return
         for i, c in enumerate(self.ops):
             if type(c) is not ConvOp or c.stem_input is not None:
@@ -874,7 +877,7 @@ class Plan:
             # 3x3 consumers transform every input element once per tap (im2col A tiles): measured
             # slower than the affine pass they replace (YOLOv8-s 18.8 -> 20.5 ms/step with them,
             # profiles/r04c_pro_ab.txt); YMS_PRO=3 includes them (dev A/B)
-            if c.shape.k != 1 and os.environ.get("YMS_PRO", "1") != "3":
+            if c.shape.k != 1 and os.environ.get("YMS_PRO", "0") != "3":
                 continue
             x = c.x
             prod = None
