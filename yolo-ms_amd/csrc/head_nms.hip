@@ -989,7 +989,7 @@ __device__ __forceinline__ void gr_region(const GraphSeg& g, float4 q, float tr,
 __global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, const float* bxy, float tr, int maxc,
                                                                NmsWs ws) {
   __shared__ int s_hist[NMS_GR_MAXN + 1];
-  __shared__ float s_red[6][16];
+  __shared__ float s_red[7][16];
   __shared__ int s_wsum[16];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int ngr = ws.gl[0];
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, co
     uint64_t key[8];
     float4 q[8];
     bool val[8];
-    float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f;
+    float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f, ar = 0.0f;
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
       const int e = tid + 1024 * k;
@@ -1014,23 +1014,25 @@ __global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, co
         mnx = fminf(mnx, cx); mxx = fmaxf(mxx, cx);
         mny = fminf(mny, cy); mxy = fmaxf(mxy, cy);
         wm = fmaxf(wm, q[k].z - q[k].x); hm = fmaxf(hm, q[k].w - q[k].y);
+        ar += (q[k].z - q[k].x) * (q[k].w - q[k].y);
       }
     }
     mnx = wave_min(mnx); mxx = wave_max(mxx); mny = wave_min(mny); mxy = wave_max(mxy);
-    wm = wave_max(wm); hm = wave_max(hm);
+    wm = wave_max(wm); hm = wave_max(hm); ar = wave_sum(ar);
     if (lane == 0) {
       s_red[0][wave] = mnx; s_red[1][wave] = mxx; s_red[2][wave] = mny;
-      s_red[3][wave] = mxy; s_red[4][wave] = wm; s_red[5][wave] = hm;
+      s_red[3][wave] = mxy; s_red[4][wave] = wm; s_red[5][wave] = hm; s_red[6][wave] = ar;
     }
     for (int i = tid; i <= NMS_GR_MAXN; i += 1024) s_hist[i] = 0;
     __syncthreads();
     GraphSeg g;
     {
       mnx = s_red[0][0]; mxx = s_red[1][0]; mny = s_red[2][0]; mxy = s_red[3][0]; wm = s_red[4][0]; hm = s_red[5][0];
+      ar = s_red[6][0];
       for (int w = 1; w < 16; ++w) {
         mnx = fminf(mnx, s_red[0][w]); mxx = fmaxf(mxx, s_red[1][w]);
         mny = fminf(mny, s_red[2][w]); mxy = fmaxf(mxy, s_red[3][w]);
-        wm = fmaxf(wm, s_red[4][w]); hm = fmaxf(hm, s_red[5][w]);
+        wm = fmaxf(wm, s_red[4][w]); hm = fmaxf(hm, s_red[5][w]); ar += s_red[6][w];
       }
       const bool any = mnx <= mxx;
       const float sx = any ? mxx - mnx : 0.0f, sy = any ? mxy - mny : 0.0f;
@@ -1046,12 +1048,18 @@ __global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, co
       g.invy = sy > 0.0f ? (float)gy / sy : 0.0f;
       g.wmax = wm; g.hmax = hm; g.gx = gx; g.gy = gy;
       g.b = b; g.c = c; g.off = off; g.n = n;
-      // expected candidates per box: the boxes whose centres fall in a search square of the
-      // largest radius; dense segments (many overlaps per box) go to the big-segment kernels,
-      // whose kept-list greedy tests only kept boxes
+      // Route: the graph kernels pay per candidate pair (centres inside the search square of the
+      // largest radius) and win when few candidates suppress each other (many boxes kept, where
+      // the kept-list greedy's lists grow long); dense, strongly overlapping segments go to the
+      // big-segment kernels.  Estimates over the segment's density: candidates per box, and
+      // suppressing neighbours per box for equal boxes of the mean area (the IoU > t region of
+      // two equal w x h boxes covers 4((1-c) + c ln c) w h of centre offsets, c = 2t / (1 + t)).
       const float rx = 2.0f * wm * (1.0f - tr), ry = 2.0f * hm * (1.0f - tr);
       const float dens = (float)n / ((sx + rx) * (sy + ry) + 1e-30f);
-      g.pad0 = (maxc > 0 && dens * rx * ry > (float)maxc) ? 1 : 0;
+      const float cc = 2.0f * tr / (1.0f + tr);
+      const float reg = 4.0f * ((1.0f - cc) + (cc > 0.0f ? cc * logf(cc) : 0.0f));
+      const float nb = dens * reg * ar / (float)max(1, n);
+      g.pad0 = (maxc > 0 && (dens * rx * ry > (float)maxc || nb > 0.125f * (float)maxc)) ? 1 : 0;
     }
     if (g.pad0) {                        // block-uniform
       if (tid == 0) {
