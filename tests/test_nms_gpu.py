@@ -12,19 +12,25 @@ from yms import ops
 pytestmark = pytest.mark.gpu
 
 
-@pytest.fixture(params=["default", "graph", "nograph"], autouse=True)
+@pytest.fixture(params=["default", "graph", "nograph", "legacy"], autouse=True)
 def nms_route(request, monkeypatch):
-    """Every case runs three ways: the default routing (graph kernels for segments of >= 2048 finite
-    boxes whose expected candidates per box are <= 256, the dense rest to the big-segment kernels),
-    the graph kernels on every segment of >= 128 finite boxes (YMS_NMS_GRAPH_MIN=128,
-    YMS_NMS_GRAPH_MAXC=0), and without them (YMS_NMS_GRAPH_MIN=0: class / big-segment kernels)."""
-    monkeypatch.delenv("YMS_NMS_GRAPH_MIN", raising=False)
-    monkeypatch.delenv("YMS_NMS_GRAPH_MAXC", raising=False)
+    """Every case runs four ways: the default routing (graph kernels for segments of >= 2048 finite
+    boxes with few expected overlaps, the rest of the big segments sorted and resolved by the
+    window-grid greedy when finite and <= 7168 boxes, else by the kept-list greedy); the graph
+    kernels on every segment of >= 128 finite boxes (YMS_NMS_GRAPH_MIN=128, YMS_NMS_GRAPH_MAXC=0);
+    no graph kernels (YMS_NMS_GRAPH_MIN=0: every big segment to the window-grid / kept-list
+    greedy); and the round-3 kernels only (also YMS_NMS_WGRID=0, YMS_NMS_CAP=1024: segments of up
+    to 1024 boxes in the class kernel, not the default 256)."""
+    for k in ("YMS_NMS_GRAPH_MIN", "YMS_NMS_GRAPH_MAXC", "YMS_NMS_WGRID", "YMS_NMS_CAP"):
+        monkeypatch.delenv(k, raising=False)
     if request.param == "graph":
         monkeypatch.setenv("YMS_NMS_GRAPH_MIN", "128")
         monkeypatch.setenv("YMS_NMS_GRAPH_MAXC", "0")
-    elif request.param == "nograph":
+    elif request.param in ("nograph", "legacy"):
         monkeypatch.setenv("YMS_NMS_GRAPH_MIN", "0")
+        if request.param == "legacy":
+            monkeypatch.setenv("YMS_NMS_WGRID", "0")
+            monkeypatch.setenv("YMS_NMS_CAP", "1024")
     return request.param
 
 
@@ -305,7 +311,7 @@ def test_graph_nms_edge_cases(monkeypatch, nms_route):
     beyond their 254-entry capacity (identical boxes: the full-rectangle rescan), long suppression
     chains (one decision round per link), mixed tiny / huge boxes (search rectangles spanning the
     grid), degenerate boxes mixed in, all centres equal, thresholds 0 / 0.999 / 1, exact ties."""
-    if nms_route == "nograph":
+    if nms_route in ("nograph", "legacy"):
         pytest.skip("graph kernels forced on below")
     monkeypatch.setenv("YMS_NMS_GRAPH_MIN", "32")
     # "graph": every segment on the graph kernels; "default": dense ones (the identical boxes, the

@@ -28,7 +28,7 @@ sets = [("level segments 6400/1600/400 (B=32, bench regime)", _level_segments(B,
         ("dense random-init-like (B=32, ~105/class)", dense),
         ("clustered (B=32, 20x30 boxes)", clustered(B, nc)),
         ("single class nc=1 (B=32, 8400 cand)", one)]
-for gmin in os.environ.get("YMS_NMSB_GMIN", "128,0").split(","):
+for gmin in os.environ.get("YMS_NMSB_GMIN", "2048,0").split(","):
     os.environ["YMS_NMS_GRAPH_MIN"] = gmin
     for name, pred in sets:
         t, k = timeit(pred)
