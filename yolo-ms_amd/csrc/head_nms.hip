@@ -368,9 +368,10 @@ __device__ __forceinline__ bool iou_gt_f(const float4& i, const float4& j, float
   return ovr > thr_f;
 }
 
-// Ascending bitonic sort of keys[0, n), n <= 8192, by one 1024-thread block.  Thread t keeps
-// keys [8t, 8t + 8) in registers: exchange distances below 8 are in-thread, below 512 lane
-// shuffles, only the rest (10 of the 91 passes at 8192 keys) go through LDS.  Padding = ~0.
+// Ascending bitonic sort of keys[0, n), n <= 8192, by one 1024-thread block; keys must have room
+// for 8192 entries (the LDS exchange passes use all of it).  Thread t keeps keys [8t, 8t + 8) in
+// registers: exchange distances below 8 are in-thread, below 512 lane shuffles, only the rest (10
+// of the 91 passes at 8192 keys) go through LDS.  Padding = ~0.
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
   const uint32_t lo = (uint32_t)__shfl_xor((int)(uint32_t)v, m);
   const uint32_t hi = (uint32_t)__shfl_xor((int)(uint32_t)(v >> 32), m);
@@ -401,14 +402,17 @@ __device__ void sort8192(uint64_t* keys, int n) {
     for (int j = k >> 1; j > 0; j >>= 1) {
       const int m = (j == (k >> 1)) ? (k - 1) : j;   // partner index = e ^ m
       if (m >= 512) {
+        // exchange through LDS in a lane-major layout (element 8t + i at i * 1024 + t): a wave's
+        // 64 accesses are a permutation of 64 consecutive 8-byte words (element-major 8t + i put
+        // 16 lanes on each bank); the partner e ^ m sits at ((e ^ m) & 7) * 1024 + ((e ^ m) >> 3)
         __syncthreads();
 #pragma unroll
-        for (int i = 0; i < 8; ++i) keys[8 * tid + i] = r[i];
+        for (int i = 0; i < 8; ++i) keys[i * 1024 + tid] = r[i];
         __syncthreads();
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
           const int e = 8 * tid + i, pe = e ^ m;
-          const uint64_t o = keys[pe];
+          const uint64_t o = keys[(pe & 7) * 1024 + (pe >> 3)];
           r[i] = (e < pe) == (o < r[i]) ? o : r[i];
         }
       } else if (m >= 8) {
@@ -502,7 +506,12 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
     uint64_t* tmp = reinterpret_cast<uint64_t*>(ws.gboxes + (long)b * A + off);   // 2n keys of room
     const uint64_t* keys;
     if (n <= NMS_CHUNK) {
-      for (int i = tid; i < n; i += 1024) s_big[i] = gk[i];
+      uint64_t kv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) kv[k] = tid + 1024 * k < n ? gk[tid + 1024 * k] : 0ull;
+#pragma unroll
+      for (int k = 0; k < 8; ++k)
+        if (tid + 1024 * k < n) s_big[tid + 1024 * k] = kv[k];
       __syncthreads();
       sort8192(s_big, n);
       keys = s_big;
@@ -531,10 +540,24 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
     float4* boxes = ws.gboxes + (long)b * A + off;
     const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
     int* idx = ws.scratch + (long)b * A + off;
-    for (int i = tid; i < n; i += 1024) {
-      const uint32_t a = (uint32_t)keys[i];
-      boxes[i] = bx[a];
-      idx[i] = (int)a;
+    for (int i0 = 0; i0 < n; i0 += 8192) {        // the gathers of 8 boxes per thread in flight together
+      uint32_t av[8];
+      float4 bv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + tid + 1024 * k;
+        av[k] = i < n ? (uint32_t)keys[i] : 0u;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + tid + 1024 * k;
+        bv[k] = i < n ? bx[av[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int i = i0 + tid + 1024 * k;
+        if (i < n) { boxes[i] = bv[k]; idx[i] = (int)av[k]; }
+      }
     }
     __syncthreads();
   }
