@@ -1412,13 +1412,14 @@ __global__ __launch_bounds__(1024) void nms_graph_resolve_kernel(int A, int nc, 
 // Window-grid greedy for sorted big segments of at most NMS_WG_MAX finite boxes, threshold >= 0
 // (the default for those; nms_big_greedy_kernel keeps the rest).  The block holds the segment's
 // sorted boxes in LDS, bins the positive-area ones by centre on a grid of cells, and repeats:
-//   1. wave 0 takes the first 64 entries of the alive list (priority order) as the window and
-//      resolves them serially among themselves: a member survives unless a kept member before it
-//      overlaps it (greedy order); survivors are appended to the keep list;
+//   1. the window = the first 64 alive boxes after the cursor (one block-wide scan of the alive
+//      bit words); the 64 x 64 suppression bits among its members are computed in parallel (one
+//      ballot per row) and resolved serially on the bit rows: a member survives unless a kept
+//      member before it overlaps it (greedy order); survivors are appended to the keep list;
 //   2. every wave takes window survivors and clears the alive bit of every later box in the cells
 //      of the survivor's search rectangle with iou_gt_f(survivor, box) (the graph kernels' radius
 //      bound: a suppressed box's centre lies inside the rectangle);
-//   3. the alive list is rebuilt (order-preserving compaction of the entries after the window).
+//   3. the cursor moves past the window.
 // Every window member has survived every box kept before it (step 2 of the earlier windows), so
 // each member's fate is that of sequential greedy NMS; the keep list comes out in priority order.
 // Work is (kept boxes x rectangle candidates) plus one serial 64-step resolve per window, so a
@@ -1433,15 +1434,23 @@ constexpr size_t NMS_WG_LDS = (size_t)NMS_WG_MAX * 16 + (size_t)NMS_WG_MAX * 4 +
 __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float thr_f, float tr, NmsWs ws) {
   extern __shared__ float4 s_box[];                                   // [NMS_WG_MAX] sorted boxes
   uint16_t* s_items = reinterpret_cast<uint16_t*>(s_box + NMS_WG_MAX);  // [NMS_WG_MAX] cell-binned
-  uint16_t* s_list = s_items + NMS_WG_MAX;                             // [NMS_WG_MAX] alive list
-  int* s_cst = reinterpret_cast<int*>(s_list + NMS_WG_MAX);            // [CELLS + 1] cell starts
+  uint16_t* s_kept = s_items + NMS_WG_MAX;                             // [NMS_WG_MAX] keep list
+  int* s_cst = reinterpret_cast<int*>(s_kept + NMS_WG_MAX);            // [CELLS + 1] cell starts
   int* s_cur = s_cst + NMS_WG_CELLS + 1;                               // [CELLS + 1] cursors
   uint32_t* s_alive = reinterpret_cast<uint32_t*>(s_cur + NMS_WG_CELLS + 1);
   __shared__ float s_red[6][16];
   __shared__ int s_wsum[16];
-  __shared__ int s_bad, s_nl, s_nk, s_nwk, s_cut;
-  __shared__ int s_wk[64];
+  __shared__ int s_bad, s_nk, s_nwk, s_cut;
+  __shared__ int s_wk[64], s_win[64];
+  __shared__ unsigned long long s_wm[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+#ifdef YMS_NMS_PROF
+  long long wacc[5] = {0, 0, 0, 0, 0}, wpt = 0;
+  int nwin = 0;
+#define WMARK(k) do { if (tid == 0) { const long long q_ = clock64(); wacc[k] += q_ - wpt; wpt = q_; } } while (0)
+#else
+#define WMARK(k) do {} while (0)
+#endif
   const int nbig = ws.big[0];
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
@@ -1452,6 +1461,10 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
     int* idx = ws.scratch + (long)b * A + off;
     if (tid == 0) { s_bad = 0; s_nk = 0; }
     __syncthreads();
+#ifdef YMS_NMS_PROF
+    if (tid == 0) wpt = clock64();
+    nwin = 0;
+#endif
     float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f;
     bool bad = false;
     constexpr int PER = (NMS_WG_MAX + 1023) / 1024;
@@ -1506,6 +1519,7 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
       g.wmax = wm; g.hmax = hm; g.gx = gx; g.gy = gy;
     }
     const int ncell = g.gx * g.gy;
+    WMARK(0);
     // bin the positive-area boxes by centre (non-positive-area boxes never suppress or get suppressed)
     for (int i = tid; i < n; i += 1024) {
       const float4 q = s_box[i];
@@ -1535,39 +1549,80 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
       if (q.z > q.x && q.w > q.y)
         s_items[atomicAdd(&s_cur[gr_cell(0.5f * (q.y + q.w), g.oy, g.invy, g.gy) * g.gx +
                                  gr_cell(0.5f * (q.x + q.z), g.ox, g.invx, g.gx)], 1)] = (uint16_t)i;
-      s_list[i] = (uint16_t)i;
     }
-    if (tid == 0) s_nl = n;
+    if (tid == 0) s_cut = -1;
     __syncthreads();
+    WMARK(1);
+    const int nwords = (n + 31) >> 5;                 // <= NMS_WG_MAX / 32 = 224 < 1024
     for (;;) {
-      const int nl = s_nl;
-      if (nl == 0) break;
-      const int m = min(64, nl);
-      if (wave == 0) {
-        const int i = lane < m ? (int)s_list[lane] : 0;
-        const float4 bi = s_box[i];
-        const int ai = lane < m ? idx[i] : 0;
-        bool alive = lane < m;
-        for (int t = 0; t < m; ++t) {
-          if (!((__ballot(alive) >> t) & 1ull)) continue;
-          float4 bt;
-          bt.x = rl_f(bi.x, t); bt.y = rl_f(bi.y, t); bt.z = rl_f(bi.z, t); bt.w = rl_f(bi.w, t);
-          if (alive && lane > t && iou_gt_f(bt, bi, thr_f, false)) alive = false;
-        }
-        const unsigned long long km = __ballot(alive);
-        const int pos = __popcll(km & ((1ull << lane) - 1ull));
-        const int nk = s_nk;
-        if (alive) {
-          idx[nk + pos] = ai;            // nk + pos <= i: entries at or after i are read above
-          s_wk[pos] = i;
-        }
-        if (lane == 0) {
-          s_nk = nk + __popcll(km);
-          s_nwk = __popcll(km);
-          s_cut = s_list[m - 1];
+      // window: the first 64 alive boxes after the cursor (block-wide scan of the alive words)
+      const int cut0 = s_cut;
+      uint32_t word = 0u;
+      if (tid < nwords) {
+        word = s_alive[tid];
+        const int lo = cut0 + 1;                      // first index still to take
+        if ((tid + 1) * 32 <= lo) word = 0u;
+        else if (tid * 32 < lo) word &= ~0u << (lo - tid * 32);
+      }
+      const int pc = __popc(word);
+      int incl = pc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      if (lane == 63 && wave < 4) s_wsum[wave] = incl;
+      __syncthreads();
+      int wb = 0, tot = 0;
+      for (int w = 0; w < 4; ++w) { if (w < wave) wb += s_wsum[w]; tot += s_wsum[w]; }
+      const int m = min(64, tot);
+      if (m == 0) break;                              // block-uniform
+#ifdef YMS_NMS_PROF
+      ++nwin;
+#endif
+      {
+        int pos = wb + incl - pc;
+        uint32_t wv = word;
+        while (wv && pos < 64) {
+          const int bit = __ffs(wv) - 1;
+          wv &= wv - 1u;
+          s_win[pos++] = tid * 32 + bit;
         }
       }
       __syncthreads();
+      // pairwise suppression bits of the window, one ballot per row: s_wm[t] bit l = member t
+      // (higher priority) suppresses member l > t
+      for (int t = wave; t < m; t += 16) {
+        const float4 bt = s_box[s_win[t]];
+        const bool hit = lane > t && lane < m && iou_gt_f(bt, s_box[s_win[lane < m ? lane : 0]], thr_f, false);
+        const unsigned long long row = __ballot(hit);
+        if (lane == 0) s_wm[t] = row;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        const int i = lane < m ? s_win[lane] : 0;
+        const unsigned long long rowl = lane < m ? s_wm[lane] : 0ull;
+        unsigned long long alive = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+        for (int t = 0; t < m; ++t) {                 // serial greedy on the bit rows (SALU)
+          const unsigned long long rt = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(rowl >> 32), t) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowl, t);
+          if ((alive >> t) & 1ull) alive &= ~rt;
+        }
+        const bool kept = (alive >> lane) & 1ull;
+        const int pos = __popcll(alive & ((1ull << lane) - 1ull));
+        const int nk = s_nk;
+        if (kept) {
+          s_kept[nk + pos] = (uint16_t)i;               // keep list (sorted indices) in LDS
+          s_wk[pos] = i;
+        }
+        if (lane == 0) {
+          s_nk = nk + __popcll(alive);
+          s_nwk = __popcll(alive);
+          s_cut = s_win[m - 1];
+        }
+      }
+      __syncthreads();
+      WMARK(2);
       const int nwk = s_nwk, cut = s_cut;
       for (int k = wave; k < nwk; k += 16) {
         const int u = s_wk[k];
@@ -1585,32 +1640,37 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
         }
       }
       __syncthreads();
-      // order-preserving compaction of the alive entries after the window, in chunks of 1024
-      int wr = 0;
-      for (int c0 = m; c0 < nl; c0 += 1024) {
-        const int e = c0 + tid;
-        const int j = e < nl ? (int)s_list[e] : 0;
-        const bool keep = e < nl && ((s_alive[j >> 5] >> (j & 31)) & 1u);
-        const unsigned long long bm = __ballot(keep);
-        if (lane == 0) s_wsum[wave] = __popcll(bm);
-        __syncthreads();
-        int wb = wr;
-        for (int w = 0; w < wave; ++w) wb += s_wsum[w];
-        int tot = 0;
-        for (int w = 0; w < 16; ++w) tot += s_wsum[w];
-        if (keep) s_list[wb + __popcll(bm & ((1ull << lane) - 1ull))] = (uint16_t)j;
-        wr += tot;
-        __syncthreads();
-      }
-      if (tid == 0) s_nl = wr;
-      __syncthreads();
+      WMARK(3);
     }
+    {
+      // keep list -> anchor ids, in place over idx (all reads before the barrier, then the writes)
+      const int nk = s_nk;
+      int av[NMS_WG_MAX / 1024];
+#pragma unroll
+      for (int k = 0; k < NMS_WG_MAX / 1024; ++k) {
+        const int e = tid + 1024 * k;
+        av[k] = e < nk ? idx[s_kept[e]] : 0;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int k = 0; k < NMS_WG_MAX / 1024; ++k) {
+        const int e = tid + 1024 * k;
+        if (e < nk) idx[e] = av[k];
+      }
+    }
+#ifdef YMS_NMS_PROF
+    if (tid == 0 && b < 2)
+      printf("WGRIDPROF b=%d c=%d n=%d kept=%d windows=%d gx=%d gy=%d load=%lld bin=%lld resolve=%lld suppress=%lld compact=%lld\n",
+             b, c, n, s_nk, nwin, g.gx, g.gy, wacc[0], wacc[1], wacc[2], wacc[3], wacc[4]);
+    for (int k = 0; k < 5; ++k) wacc[k] = 0;
+#endif
     if (tid == 0) {
       ws.cls_cnt[(long)b * nc + c] = s_nk;
       ws.route[(long)b * nc + c] = 2;                 // done: the kept-list greedy skips it
     }
     __syncthreads();
   }
+#undef WMARK
 }
 
 __global__ void nms_compact_kernel(int A, int nc, NmsWs ws, int64_t* keep_idx, int* keep_lbl,
