@@ -1503,8 +1503,10 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   // round trip at `ratio` x the algorithmic bytes, keeping at least `min_blocks` workgroups.
   // (interleaved A/B, YOLOv8-s step: off 19.71/19.71/19.81 ms, ratio 1 19.62/19.64/19.76 ms;
   // YOLO-MS-S 40.11/40.12 -> 40.04/40.02 ms -- the wgrads run on the side stream, so the
-  // step gains only the HBM contention the slabs caused)
-  static const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 1.0;
+  // step gains only the HBM contention the slabs caused).  Round 4: the step keeps improving down
+  // to ~0.05, where min_blocks binds (YOLOv8-s 18.23 -> 17.93 ms, YOLO-MS-S 36.22 -> 35.66 ms;
+  // profiles/r04ad_wgrad_slab_ratio_ab.txt): fewer, longer side-stream blocks and ~no slab bytes.
+  static const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;
   static const int min_blocks = getenv("YMS_WG_MIN_BLOCKS") ? std::max(1, atoi(getenv("YMS_WG_MIN_BLOCKS"))) : 256;
   if (ratio > 0.0) {
     const double data = (double)M * (double)(rup(s->cout, 8) + w.cin8) * es;

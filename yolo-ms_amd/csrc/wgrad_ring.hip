@@ -248,7 +248,7 @@ bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
   int splits = std::max(1, std::min(cdiv(q.nkt, 8), cdiv((long)bpc * conv_cu_count(), blocks)));
   const double data = (double)M * (double)(rup(s->cout, 8) + q.cin8) * 2.0;
   const double slab_rt = 2.0 * 4.0 * (double)q.slab_rows * (double)q.slab_ld;
-  const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 1.0;   // dev A/B
+  const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;   // see conv_igemm.hip
   const int cap = std::max((int)(ratio * data / slab_rt), cdiv(256, blocks));
   splits = std::max(1, std::min(splits, cap));
   q.kt_per_split = cdiv(q.nkt, splits);
