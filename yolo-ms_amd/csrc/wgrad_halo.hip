@@ -286,7 +286,7 @@ bool wgrad_halo_plan(const yms_conv_shape* s, WHPlan* w) {
   int splits = std::max(1, std::min(q.npatch, cdiv((long)bpc * conv_cu_count(), tiles)));
   const double data = (double)s->n * s->ho * s->wo * rup(s->cout, 8) * 2.0 + (double)s->n * s->h * s->w * cin8 * 2.0;
   const double slab_rt = 2.0 * 4.0 * (double)q.slab_rows * q.slab_ld * q.wk;
-  const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 1.0;   // dev A/B
+  const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;   // see conv_igemm.hip
   const int cap = std::max((int)(ratio * data / slab_rt), cdiv(256, tiles));
   splits = std::max(1, std::min(splits, cap));
   q.pps = cdiv(q.npatch, splits);

@@ -249,7 +249,8 @@ bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
   const double data = (double)M * (double)(rup(s->cout, 8) + q.cin8) * 2.0;
   const double slab_rt = 2.0 * 4.0 * (double)q.slab_rows * (double)q.slab_ld;
   const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;   // see conv_igemm.hip
-  const int cap = std::max((int)(ratio * data / slab_rt), cdiv(256, blocks));
+  const int minb = std::max(1, env_int_wr("YMS_WG_RING_MINB", 256));   // dev A/B (read per call)
+  const int cap = std::max((int)(ratio * data / slab_rt), cdiv(minb, blocks));
   splits = std::max(1, std::min(splits, cap));
   q.kt_per_split = cdiv(q.nkt, splits);
   q.splits = cdiv(q.nkt, q.kt_per_split);
