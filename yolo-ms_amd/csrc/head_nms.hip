@@ -215,12 +215,20 @@ __global__ __launch_bounds__(1024) void nms_bucket_kernel(int A, int nc, const f
   const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
   for (int c = threadIdx.x; c < 3 * nc; c += blockDim.x) s_cnt[c] = 0;
   __syncthreads();
-  for (int a = threadIdx.x; a < A; a += blockDim.x) {
-    const int l = lab ? lab[a] : 0;
-    if (l >= 0) {
+  const int lane = threadIdx.x & 63;
+  for (int a0 = 0; a0 < A; a0 += blockDim.x) {       // block-uniform trip count (wave ballots below)
+    const int a = a0 + (int)threadIdx.x;
+    const int l = a < A ? (lab ? lab[a] : 0) : -1;
+    // one class per wave is the common case (a pyramid level's anchors share the arg-max class
+    // of a random-init head; nc = 1): one atomic for the wave instead of 64 on one LDS word
+    const unsigned long long vm = __ballot(l >= 0);
+    const int lref = vm ? __shfl(l, __ffsll((long long)vm) - 1) : -1;
+    if (vm && __ballot(l >= 0 && l != lref) == 0ull) {
+      if (lane == 0) atomicAdd(&s_cnt[lref], __popcll(vm));
+    } else if (l >= 0) {
       atomicAdd(&s_cnt[l], 1);
-      if (gmin > 0 && !box_ok(bx[a])) s_bad[l] = 1;
     }
+    if (l >= 0 && gmin > 0 && !box_ok(bx[a])) s_bad[l] = 1;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -246,11 +254,21 @@ __global__ __launch_bounds__(1024) void nms_bucket_kernel(int A, int nc, const f
   }
   __syncthreads();
   uint64_t* keys = ws.gkeys + (long)b * A;
-  for (int a = threadIdx.x; a < A; a += blockDim.x) {
-    const int l = lab ? lab[a] : 0;
-    if (l < 0) continue;
-    const int pos = atomicAdd(&s_cur[l], 1);
-    keys[pos] = ((uint64_t)(~orderable(sc[a])) << 32) | (uint32_t)a;
+  for (int a0 = 0; a0 < A; a0 += blockDim.x) {
+    const int a = a0 + (int)threadIdx.x;
+    const int l = a < A ? (lab ? lab[a] : 0) : -1;
+    const unsigned long long vm = __ballot(l >= 0);
+    if (!vm) continue;                                 // wave-uniform
+    const int lref = __shfl(l, __ffsll((long long)vm) - 1);
+    int pos;
+    if (__ballot(l >= 0 && l != lref) == 0ull) {       // bucket order is irrelevant (keys are a total order)
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&s_cur[lref], __popcll(vm));
+      pos = __shfl(base, 0) + __popcll(vm & ((1ull << lane) - 1ull));
+    } else {
+      pos = l >= 0 ? atomicAdd(&s_cur[l], 1) : 0;
+    }
+    if (l >= 0) keys[pos] = ((uint64_t)(~orderable(sc[a])) << 32) | (uint32_t)a;
   }
 }
 
