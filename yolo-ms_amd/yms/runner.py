@@ -293,14 +293,23 @@ def run(module, inputs, grad_hook=None):
         return plan, list(outs)
     # eval / inference: no autograd graph, eval-cached packed weights + folded BN
     stream = L.stream_ptr(dev)
+    decode = isinstance(plan.kind, tuple) and plan.kind[0] == "decode"
     with torch.no_grad():
-        arena = plan.new_arena(dev, stream)
+        # a decode plan returns a fresh tensor, so its arena is internal: keep it per stream (the
+        # next call on that stream is ordered after this one) and skip re-zeroing the pad ranges
+        cached = getattr(plan, "_infer_arena", None) if decode else None
+        if cached is not None and cached[0] == stream and cached[1].device == dev:
+            arena = cached[1]
+        else:
+            arena = plan.new_arena(dev, stream)
+            if decode:
+                plan._infer_arena = (stream, arena)
         rt = Rt(plan, arena.data_ptr(), stream, False)
         rt.eval_base = plan.ensure_eval_cache(dev, stream)
         _load_inputs(plan, rt, inputs)
         for op in plan.ops:
             op.fwd(rt)
-        if isinstance(plan.kind, tuple) and plan.kind[0] == "decode":
+        if decode:
             return plan, [_decode(plan, rt, arena)]
         return plan, _outputs(plan, arena, dtype)
 
