@@ -319,3 +319,35 @@ def test_wgrad_ring(shp, dt, var, monkeypatch):
         got = dw.double().cpu() - (0.25 if acc else 0.0)
         rel = ((got - ref).norm() / ref.norm()).item()
         assert rel < 1e-5 and (got - ref).abs().max().item() <= 1e-5 * ref.abs().max().item() + 1e-6, (acc, rel)
+
+
+@pytest.mark.parametrize("route", ["tt", "ring", "halo"])
+@pytest.mark.parametrize("ratio", ["0.05", "1.0", "0"])
+def test_wgrad_split_k_slab_cap(route, ratio, monkeypatch):
+    """The split-K slab cap (YMS_WG_SLAB_RATIO: default 0.05 of the layer's x + dz bytes; 1.0 the
+    round-3 default; 0 uncapped) changes only how many fp32 partial slabs the weight gradient sums
+    in its fixed-order reduce: every setting on every wgrad kernel (register-staged TT, LDS-DMA ring,
+    halo-staged 3x3) matches the fp32 torch gradient on bf16 operands, on layers deep enough in
+    pixels (B*H*W up to 32k) that the split count differs between the settings."""
+    monkeypatch.setenv("YMS_WG_SLAB_RATIO", ratio)
+    monkeypatch.setenv("YMS_WG_RING", "1" if route == "ring" else "0")
+    monkeypatch.setenv("YMS_WG_HALO", "1" if route == "halo" else "0")
+    dtype = torch.bfloat16
+    cases = [(8, 64, 40, 40, 64, 3, 1), (8, 128, 20, 20, 256, 1, 1), (4, 32, 80, 80, 32, 3, 1),
+             (8, 96, 40, 40, 128, 3, 2)]
+    for n, cin, h, w, cout, k, s in cases:
+        g = torch.Generator().manual_seed(n + cin + cout + k)
+        x = torch.randn(n, cin, h, w, generator=g)
+        shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+        dz = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+        xr = x.to(dtype).float()
+        wr = torch.zeros(cout, cin, k, k, requires_grad=True)
+        F.conv2d(xr, wr, None, s, k // 2).backward(dz.to(dtype).float())
+        sp = ctypes.pointer(shp_)
+        xb, dzb = nhwc(x, dtype), nhwc(dz, dtype)
+        wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device="cuda")
+        dw = torch.zeros(cout, cin, k, k, device="cuda")
+        L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0,
+               ws.data_ptr(), wsb, dw.data_ptr(), 0, L.stream_ptr())
+        _close(dw.cpu(), wr.grad, 2e-3)

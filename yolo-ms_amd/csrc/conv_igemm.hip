@@ -1506,8 +1506,9 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   // step gains only the HBM contention the slabs caused).  Round 4: the step keeps improving down
   // to ~0.05, where min_blocks binds (YOLOv8-s 18.23 -> 17.93 ms, YOLO-MS-S 36.22 -> 35.66 ms;
   // profiles/r04ad_wgrad_slab_ratio_ab.txt): fewer, longer side-stream blocks and ~no slab bytes.
-  static const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;
-  static const int min_blocks = getenv("YMS_WG_MIN_BLOCKS") ? std::max(1, atoi(getenv("YMS_WG_MIN_BLOCKS"))) : 256;
+  // (read per call, as the ring / halo kernels do: tests switch them at run time)
+  const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;
+  const int min_blocks = getenv("YMS_WG_MIN_BLOCKS") ? std::max(1, atoi(getenv("YMS_WG_MIN_BLOCKS"))) : 256;
   if (ratio > 0.0) {
     const double data = (double)M * (double)(rup(s->cout, 8) + w.cin8) * es;
     const double slab_rt = 2.0 * 4.0 * (double)w.slab_rows * (double)w.slab_ld;
