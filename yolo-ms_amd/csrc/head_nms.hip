@@ -205,15 +205,13 @@ __device__ __forceinline__ bool box_ok(float4 q) {
 // gmin..NMS_GR_MAXN boxes whose coordinates are all finite (|v| < 1e15) go to the graph kernels
 // (gmin = 0: none), the rest of those above NMS_CAP to the big-segment kernels.
 __global__ __launch_bounds__(1024) void nms_bucket_kernel(int A, int nc, const float* score, const int* label,
-                                                          const float* bxy, int gmin, int cap, NmsWs ws) {
-  extern __shared__ int s_cnt[];      // [nc] counts, [nc] cursors, [nc] non-finite flags
+                                                          int gmin, int cap, NmsWs ws) {
+  extern __shared__ int s_cnt[];      // [nc] counts, [nc] cursors
   int* s_cur = s_cnt + nc;
-  int* s_bad = s_cur + nc;
   const int b = blockIdx.x;
   const int* lab = label ? label + (long)b * A : nullptr;
   const float* sc = score + (long)b * A;
-  const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
-  for (int c = threadIdx.x; c < 3 * nc; c += blockDim.x) s_cnt[c] = 0;
+  for (int c = threadIdx.x; c < 2 * nc; c += blockDim.x) s_cnt[c] = 0;
   __syncthreads();
   const int lane = threadIdx.x & 63;
   for (int a0 = 0; a0 < A; a0 += blockDim.x) {       // block-uniform trip count (wave ballots below)
@@ -228,7 +226,6 @@ __global__ __launch_bounds__(1024) void nms_bucket_kernel(int A, int nc, const f
     } else if (l >= 0) {
       atomicAdd(&s_cnt[l], 1);
     }
-    if (l >= 0 && gmin > 0 && !box_ok(bx[a])) s_bad[l] = 1;
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -238,13 +235,11 @@ __global__ __launch_bounds__(1024) void nms_bucket_kernel(int A, int nc, const f
       s_cur[c] = run;
       ws.cls_off[(long)b * nc + c] = run;
       ws.cls_cnt[(long)b * nc + c] = k;    // candidates (rewritten with kept count by the NMS pass)
-      const bool graph = gmin > 0 && k >= gmin && k <= NMS_GR_MAXN && !s_bad[c];
-      ws.route[(long)b * nc + c] = graph ? 1 : 0;
-      if (graph) {
-        const int slot = atomicAdd(ws.gl, 1);
-        ws.gl[3 + 2 * slot] = b;
-        ws.gl[4 + 2 * slot] = c;
-      } else if (k > cap) {
+      // big path (route 3): above the class kernel's cap, or a graph candidate (the window-grid
+      // kernel routes it on its box statistics); the class kernel takes the rest (route 0)
+      const bool big = k > cap || (gmin > 0 && k >= gmin && k <= NMS_GR_MAXN);
+      ws.route[(long)b * nc + c] = big ? 3 : 0;
+      if (big) {
         const int slot = atomicAdd(ws.big, 1);
         ws.big[1 + 2 * slot] = b;
         ws.big[2 + 2 * slot] = c;
@@ -482,7 +477,7 @@ __global__ __launch_bounds__(1024) void nms_chunk_sort_kernel(int A, int nc, Nms
     const int sg = it / nch, ch = it % nch;
     const int b = ws.big[1 + 2 * sg], c = ws.big[2 + 2 * sg];
     const int n = ws.cls_cnt[(long)b * nc + c];
-    if (n <= NMS_CHUNK || ch * NMS_CHUNK >= n) continue;    // block-uniform
+    if (ws.route[(long)b * nc + c] != 3 || n <= NMS_CHUNK || ch * NMS_CHUNK >= n) continue;    // block-uniform
     uint64_t* gk = ws.gkeys + (long)b * A + ws.cls_off[(long)b * nc + c] + (long)ch * NMS_CHUNK;
     const int len = min(NMS_CHUNK, n - ch * NMS_CHUNK);
     for (int i = threadIdx.x; i < len; i += 1024) s_big[i] = gk[i];
@@ -519,6 +514,7 @@ __global__ __launch_bounds__(1024) void nms_big_sort_kernel(int A, int nc, const
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
     const int n = ws.cls_cnt[(long)b * nc + c];
+    if (ws.route[(long)b * nc + c] != 3) continue;     // block-uniform: graph / window-grid segments
     const int off = ws.cls_off[(long)b * nc + c];
     uint64_t* gk = ws.gkeys + (long)b * A + off;
     uint64_t* tmp = reinterpret_cast<uint64_t*>(ws.gboxes + (long)b * A + off);   // 2n keys of room
@@ -647,7 +643,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
     const int n = ws.cls_cnt[(long)b * nc + c];
-    if (n <= win_max || ws.route[(long)b * nc + c] == 2) continue;   // block-uniform: window / wgrid kernels'
+    if (n <= win_max || ws.route[(long)b * nc + c] != 3) continue;   // block-uniform: window / wgrid / graph kernels'
     const int off = ws.cls_off[(long)b * nc + c];
     float4* boxes = ws.gboxes + (long)b * A + off;
     int* idx = ws.scratch + (long)b * A + off;
@@ -865,7 +861,7 @@ __global__ __launch_bounds__(1024) void nms_window_kernel(int A, int nc, float t
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
     const int n = ws.cls_cnt[(long)b * nc + c];
-    if (n > NMS_WIN_MAX || ws.route[(long)b * nc + c] == 2) continue;   // block-uniform: big greedy / wgrid
+    if (n > NMS_WIN_MAX || ws.route[(long)b * nc + c] != 3) continue;   // block-uniform: big greedy / wgrid / graph
     const int off = ws.cls_off[(long)b * nc + c];
     float4* boxes = ws.gboxes + (long)b * A + off;
     int* idx = ws.scratch + (long)b * A + off;
@@ -1027,7 +1023,7 @@ __device__ __forceinline__ void gr_region(const GraphSeg& g, float4 q, float tr,
   y1 = gr_cell(cy + ry, g.oy, g.invy, g.gy);
 }
 
-__global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, const float* bxy, float tr, int maxc,
+__global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, const float* bxy, float tr,
                                                                NmsWs ws) {
   __shared__ int s_hist[NMS_GR_MAXN + 1];
   __shared__ float s_red[7][16];
@@ -1089,29 +1085,6 @@ __global__ __launch_bounds__(1024) void nms_graph_build_kernel(int A, int nc, co
       g.invy = sy > 0.0f ? (float)gy / sy : 0.0f;
       g.wmax = wm; g.hmax = hm; g.gx = gx; g.gy = gy;
       g.b = b; g.c = c; g.off = off; g.n = n;
-      // Route: the graph kernels pay per candidate pair (centres inside the search square of the
-      // largest radius) and win when few candidates suppress each other (many boxes kept, where
-      // the kept-list greedy's lists grow long); dense, strongly overlapping segments go to the
-      // big-segment kernels.  Estimates over the segment's density: candidates per box, and
-      // suppressing neighbours per box for equal boxes of the mean area (the IoU > t region of
-      // two equal w x h boxes covers 4((1-c) + c ln c) w h of centre offsets, c = 2t / (1 + t)).
-      const float rx = 2.0f * wm * (1.0f - tr), ry = 2.0f * hm * (1.0f - tr);
-      const float dens = (float)n / ((sx + rx) * (sy + ry) + 1e-30f);
-      const float cc = 2.0f * tr / (1.0f + tr);
-      const float reg = 4.0f * ((1.0f - cc) + (cc > 0.0f ? cc * logf(cc) : 0.0f));
-      const float nb = dens * reg * ar / (float)max(1, n);
-      g.pad0 = (maxc > 0 && (dens * rx * ry > (float)maxc || nb > 0.125f * (float)maxc)) ? 1 : 0;
-    }
-    if (g.pad0) {                        // block-uniform
-      if (tid == 0) {
-        const int bs = atomicAdd(ws.big, 1);
-        ws.big[1 + 2 * bs] = b;
-        ws.big[2 + 2 * bs] = c;
-        g.n = -1;
-        ws.gseg[slot] = g;
-      }
-      __syncthreads();
-      continue;
     }
     const int ncell = g.gx * g.gy;      // + 1: the non-positive-area boxes
     int cell[8];
@@ -1320,7 +1293,6 @@ __global__ __launch_bounds__(1024) void nms_graph_resolve_kernel(int A, int nc, 
   const int ngr = ws.gl[0];
   for (int slot = blockIdx.x; slot < ngr; slot += gridDim.x) {
     const GraphSeg g = ws.gseg[slot];
-    if (g.n < 0) continue;                        // block-uniform: routed to the big-segment kernels
     const int n = g.n, nv = g.nvalid;
     const long base = (long)g.b * A + g.off;
     const float4* gb = ws.gboxes + base;
@@ -1449,14 +1421,16 @@ constexpr int NMS_WG_CELLS = NMS_WG_GMAX * NMS_WG_GMAX;
 constexpr size_t NMS_WG_LDS = (size_t)NMS_WG_MAX * 16 + (size_t)NMS_WG_MAX * 4 + (size_t)(NMS_WG_CELLS + 1) * 8 +
                               (size_t)(NMS_WG_MAX / 32) * 4;
 
-__global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float thr_f, float tr, NmsWs ws) {
+__global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const float* bxy, float thr_f, float tr,
+                                                         int gmin, int maxc, int wg_on, NmsWs ws) {
   extern __shared__ float4 s_box[];                                   // [NMS_WG_MAX] sorted boxes
+  uint64_t* s_keys = reinterpret_cast<uint64_t*>(s_box);             // [8192] keys while sorting (aliases s_box)
   uint16_t* s_items = reinterpret_cast<uint16_t*>(s_box + NMS_WG_MAX);  // [NMS_WG_MAX] cell-binned
   uint16_t* s_kept = s_items + NMS_WG_MAX;                             // [NMS_WG_MAX] keep list
   int* s_cst = reinterpret_cast<int*>(s_kept + NMS_WG_MAX);            // [CELLS + 1] cell starts
   int* s_cur = s_cst + NMS_WG_CELLS + 1;                               // [CELLS + 1] cursors
   uint32_t* s_alive = reinterpret_cast<uint32_t*>(s_cur + NMS_WG_CELLS + 1);
-  __shared__ float s_red[6][16];
+  __shared__ float s_red[7][16];
   __shared__ int s_wsum[16];
   __shared__ int s_bad, s_nk, s_nwk, s_cut;
   __shared__ int s_wk[64], s_win[64];
@@ -1473,9 +1447,10 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
     const int n = ws.cls_cnt[(long)b * nc + c];
-    if (n > NMS_WG_MAX) continue;                     // block-uniform: the kept-list greedy's
+    if (n > NMS_GR_MAXN) continue;                    // block-uniform: the big-segment kernels'
     const int off = ws.cls_off[(long)b * nc + c];
-    const float4* boxes = ws.gboxes + (long)b * A + off;
+    const uint64_t* gk = ws.gkeys + (long)b * A + off;
+    const float4* bx = reinterpret_cast<const float4*>(bxy) + (long)b * A;
     int* idx = ws.scratch + (long)b * A + off;
     if (tid == 0) { s_bad = 0; s_nk = 0; }
     __syncthreads();
@@ -1483,49 +1458,116 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
     if (tid == 0) wpt = clock64();
     nwin = 0;
 #endif
-    float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f;
+    // the segment's (unsorted) keys and boxes in registers: route statistics first
+    float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f, ar = 0.0f;
     bool bad = false;
-    constexpr int PER = (NMS_WG_MAX + 1023) / 1024;
+    constexpr int PER = NMS_GR_MAXN / 1024;
+    uint64_t kv[PER];
     float4 qv[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {              // all loads in flight before the first use
       const int i = tid + 1024 * k;
-      qv[k] = i < n ? boxes[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      kv[k] = i < n ? gk[i] : ~0ull;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 1024 * k;
+      qv[k] = i < n ? bx[(uint32_t)kv[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
     }
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
       const int i = tid + 1024 * k;
       if (i >= n) continue;
       const float4 q = qv[k];
-      s_box[i] = q;
       if (!box_ok(q)) bad = true;
       else if (q.z > q.x && q.w > q.y) {
         const float cx = 0.5f * (q.x + q.z), cy = 0.5f * (q.y + q.w);
         mnx = fminf(mnx, cx); mxx = fmaxf(mxx, cx); mny = fminf(mny, cy); mxy = fmaxf(mxy, cy);
-        wm = fmaxf(wm, q.z - q.x); hm = fmaxf(hm, q.w - q.y);
+        wm = fmaxf(wm, q.z - q.x); hm = fmaxf(hm, q.w - q.y); ar += (q.z - q.x) * (q.w - q.y);
       }
+    }
+    mnx = wave_min(mnx); mxx = wave_max(mxx); mny = wave_min(mny); mxy = wave_max(mxy);
+    wm = wave_max(wm); hm = wave_max(hm); ar = wave_sum(ar);
+    const bool wbad = __ballot(bad) != 0ull;
+    if (lane == 0) {
+      s_red[0][wave] = mnx; s_red[1][wave] = mxx; s_red[2][wave] = mny;
+      s_red[3][wave] = mxy; s_red[4][wave] = wm; s_red[5][wave] = hm; s_red[6][wave] = ar;
+      if (wbad) s_bad = 1;
+    }
+    __syncthreads();
+    mnx = s_red[0][0]; mxx = s_red[1][0]; mny = s_red[2][0]; mxy = s_red[3][0]; wm = s_red[4][0]; hm = s_red[5][0];
+    ar = s_red[6][0];
+    for (int w = 1; w < 16; ++w) {
+      mnx = fminf(mnx, s_red[0][w]); mxx = fmaxf(mxx, s_red[1][w]);
+      mny = fminf(mny, s_red[2][w]); mxy = fmaxf(mxy, s_red[3][w]);
+      wm = fmaxf(wm, s_red[4][w]); hm = fmaxf(hm, s_red[5][w]); ar += s_red[6][w];
+    }
+    const bool sbad = s_bad != 0;
+    {
+      // Route (block-uniform).  The graph kernels pay per candidate pair (centres inside the
+      // search square of the largest radius) and win when few candidates suppress each other
+      // (many boxes kept, where the greedy walks long keep lists); dense, strongly overlapping
+      // segments stay here.  Estimates over the segment's density: candidates per box, and
+      // suppressing neighbours per box for equal boxes of the mean area (the IoU > t region of two
+      // equal w x h boxes covers 4((1-c) + c ln c) w h of centre offsets, c = 2t / (1 + t)).
+      bool graph = gmin > 0 && n >= gmin && !sbad;
+      if (graph && maxc > 0) {
+        const bool any = mnx <= mxx;
+        const float sx = any ? mxx - mnx : 0.0f, sy = any ? mxy - mny : 0.0f;
+        const float rx = 2.0f * wm * (1.0f - tr), ry = 2.0f * hm * (1.0f - tr);
+        const float dens = (float)n / ((sx + rx) * (sy + ry) + 1e-30f);
+        const float cc = 2.0f * tr / (1.0f + tr);
+        const float reg = 4.0f * ((1.0f - cc) + (cc > 0.0f ? cc * logf(cc) : 0.0f));
+        const float nb = dens * reg * ar / (float)max(1, n);
+        if (dens * rx * ry > (float)maxc || nb > 0.125f * (float)maxc) graph = false;
+      }
+      if (graph) {
+        if (tid == 0) {
+          const int slot = atomicAdd(ws.gl, 1);
+          ws.gl[3 + 2 * slot] = b;
+          ws.gl[4 + 2 * slot] = c;
+          ws.route[(long)b * nc + c] = 1;
+        }
+        __syncthreads();
+        continue;
+      }
+      if (sbad || !wg_on || n > NMS_WG_MAX) {        // the kept-list greedy's (after big_sort)
+        __syncthreads();
+        continue;
+      }
+    }
+    // sort the keys in LDS (priority order), then the sorted anchors to idx and boxes to s_box
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 1024 * k;
+      if (i < n) s_keys[i] = kv[k];
+    }
+    __syncthreads();
+    sort8192(s_keys, n);                              // ends with a barrier
+    uint32_t av[PER];
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 1024 * k;
+      av[k] = i < n ? (uint32_t)s_keys[i] : 0u;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 1024 * k;
+      qv[k] = i < n ? bx[av[k]] : make_float4(0.f, 0.f, 0.f, 0.f);
+      if (i < n) idx[i] = (int)av[k];
+    }
+    __syncthreads();                                  // s_keys (aliasing s_box) fully read
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int i = tid + 1024 * k;
+      if (i < n) s_box[i] = qv[k];
     }
     for (int w = tid; w < (n + 31) / 32; w += 1024)
       s_alive[w] = (w == n / 32) ? ((1u << (n & 31)) - 1u) : 0xffffffffu;
     for (int i = tid; i <= NMS_WG_CELLS; i += 1024) s_cst[i] = 0;
-    mnx = wave_min(mnx); mxx = wave_max(mxx); mny = wave_min(mny); mxy = wave_max(mxy);
-    wm = wave_max(wm); hm = wave_max(hm);
-    const bool wbad = __ballot(bad) != 0ull;
-    if (lane == 0) {
-      s_red[0][wave] = mnx; s_red[1][wave] = mxx; s_red[2][wave] = mny;
-      s_red[3][wave] = mxy; s_red[4][wave] = wm; s_red[5][wave] = hm;
-      if (wbad) s_bad = 1;
-    }
     __syncthreads();
-    if (s_bad) { __syncthreads(); continue; }         // block-uniform: the kept-list greedy's
     GraphSeg g;
     {
-      mnx = s_red[0][0]; mxx = s_red[1][0]; mny = s_red[2][0]; mxy = s_red[3][0]; wm = s_red[4][0]; hm = s_red[5][0];
-      for (int w = 1; w < 16; ++w) {
-        mnx = fminf(mnx, s_red[0][w]); mxx = fmaxf(mxx, s_red[1][w]);
-        mny = fminf(mny, s_red[2][w]); mxy = fmaxf(mxy, s_red[3][w]);
-        wm = fmaxf(wm, s_red[4][w]); hm = fmaxf(hm, s_red[5][w]);
-      }
       const bool any = mnx <= mxx;
       const float sx = any ? mxx - mnx : 0.0f, sy = any ? mxy - mny : 0.0f;
       const float csx = fmaxf(0.5f * wm * (1.0f - tr), 1e-30f), csy = fmaxf(0.5f * hm * (1.0f - tr), 1e-30f);
@@ -1689,6 +1731,202 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, float th
     __syncthreads();
   }
 #undef WMARK
+}
+
+// The window-grid greedy for sorted segments too big for LDS (NMS_WG_MAX < n <= NMS_WGG_MAX, finite,
+// threshold >= 0: the 25,600-box level segments of a random-init model at 1280): the same windows,
+// bit-matrix resolve and cell-grid suppression as nms_wgrid_kernel, with the sorted boxes read from
+// global memory (big_sort's output, L2-resident), the cell-binned indices and the keep list in the
+// segment's slices of ws.cellst / ws.gkey2, and the alive bits and cell table in LDS.  Runs after
+// nms_big_sort_kernel; the segments it resolves (route 2) are skipped by the kept-list greedy.
+constexpr int NMS_WGG_MAX = 32768;                    // alive bits: one 32-bit word per thread
+__global__ __launch_bounds__(1024) void nms_wgrid_glb_kernel(int A, int nc, float thr_f, float tr, NmsWs ws) {
+  __shared__ uint32_t s_alive[NMS_WGG_MAX / 32];
+  __shared__ int s_cst[NMS_WG_CELLS + 1], s_cur[NMS_WG_CELLS + 1];
+  __shared__ float s_red[6][16];
+  __shared__ int s_wsum[16];
+  __shared__ int s_bad, s_nk, s_nwk, s_cut;
+  __shared__ int s_wk[64], s_win[64];
+  __shared__ float4 s_wb[64];
+  __shared__ unsigned long long s_wm[64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nbig = ws.big[0];
+  for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
+    const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
+    const int n = ws.cls_cnt[(long)b * nc + c];
+    if (ws.route[(long)b * nc + c] != 3 || n <= NMS_WG_MAX || n > NMS_WGG_MAX) continue;   // block-uniform
+    const int off = ws.cls_off[(long)b * nc + c];
+    const float4* gb = ws.gboxes + (long)b * A + off;          // sorted boxes
+    int* idx = ws.scratch + (long)b * A + off;                 // sorted anchor ids
+    int* items = ws.cellst + (long)b * (A + nc) + off + c;     // n cell-binned indices
+    int* kept = reinterpret_cast<int*>(ws.gkey2 + (long)b * A + off);   // keep list (sorted indices)
+    if (tid == 0) { s_bad = 0; s_nk = 0; s_cut = -1; }
+    __syncthreads();
+    float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f;
+    bool bad = false;
+    for (int i = tid; i < n; i += 1024) {
+      const float4 q = gb[i];
+      if (!box_ok(q)) bad = true;
+      else if (q.z > q.x && q.w > q.y) {
+        const float cx = 0.5f * (q.x + q.z), cy = 0.5f * (q.y + q.w);
+        mnx = fminf(mnx, cx); mxx = fmaxf(mxx, cx); mny = fminf(mny, cy); mxy = fmaxf(mxy, cy);
+        wm = fmaxf(wm, q.z - q.x); hm = fmaxf(hm, q.w - q.y);
+      }
+    }
+    const int nwords = (n + 31) >> 5;                 // <= 1024
+    for (int w = tid; w < nwords; w += 1024) s_alive[w] = (w == n / 32) ? ((1u << (n & 31)) - 1u) : 0xffffffffu;
+    for (int i = tid; i <= NMS_WG_CELLS; i += 1024) s_cst[i] = 0;
+    mnx = wave_min(mnx); mxx = wave_max(mxx); mny = wave_min(mny); mxy = wave_max(mxy);
+    wm = wave_max(wm); hm = wave_max(hm);
+    const bool wbad = __ballot(bad) != 0ull;
+    if (lane == 0) {
+      s_red[0][wave] = mnx; s_red[1][wave] = mxx; s_red[2][wave] = mny;
+      s_red[3][wave] = mxy; s_red[4][wave] = wm; s_red[5][wave] = hm;
+      if (wbad) s_bad = 1;
+    }
+    __syncthreads();
+    if (s_bad) { __syncthreads(); continue; }         // block-uniform: the kept-list greedy's
+    GraphSeg g;
+    {
+      mnx = s_red[0][0]; mxx = s_red[1][0]; mny = s_red[2][0]; mxy = s_red[3][0]; wm = s_red[4][0]; hm = s_red[5][0];
+      for (int w = 1; w < 16; ++w) {
+        mnx = fminf(mnx, s_red[0][w]); mxx = fmaxf(mxx, s_red[1][w]);
+        mny = fminf(mny, s_red[2][w]); mxy = fmaxf(mxy, s_red[3][w]);
+        wm = fmaxf(wm, s_red[4][w]); hm = fmaxf(hm, s_red[5][w]);
+      }
+      const bool any = mnx <= mxx;
+      const float sx = any ? mxx - mnx : 0.0f, sy = any ? mxy - mny : 0.0f;
+      const float csx = fmaxf(0.5f * wm * (1.0f - tr), 1e-30f), csy = fmaxf(0.5f * hm * (1.0f - tr), 1e-30f);
+      const int gx = (int)fminf((float)NMS_WG_GMAX, floorf(sx / csx) + 1.0f);
+      const int gy = (int)fminf((float)NMS_WG_GMAX, floorf(sy / csy) + 1.0f);
+      g.ox = any ? mnx : 0.0f; g.oy = any ? mny : 0.0f;
+      g.invx = sx > 0.0f ? (float)gx / sx : 0.0f;
+      g.invy = sy > 0.0f ? (float)gy / sy : 0.0f;
+      g.wmax = wm; g.hmax = hm; g.gx = gx; g.gy = gy;
+    }
+    const int ncell = g.gx * g.gy;
+    for (int i = tid; i < n; i += 1024) {
+      const float4 q = gb[i];
+      if (q.z > q.x && q.w > q.y)
+        atomicAdd(&s_cst[gr_cell(0.5f * (q.y + q.w), g.oy, g.invy, g.gy) * g.gx +
+                         gr_cell(0.5f * (q.x + q.z), g.ox, g.invx, g.gx)], 1);
+    }
+    __syncthreads();
+    {
+      const int v = tid <= ncell ? s_cst[tid] : 0;
+      int incl = v;
+#pragma unroll
+      for (int m = 1; m < 64; m <<= 1) {
+        const int o = __shfl_up(incl, m);
+        if (lane >= m) incl += o;
+      }
+      if (lane == 63) s_wsum[wave] = incl;
+      __syncthreads();
+      int wbase = 0;
+      for (int w = 0; w < wave; ++w) wbase += s_wsum[w];
+      if (tid <= ncell) { s_cst[tid] = wbase + incl - v; s_cur[tid] = wbase + incl - v; }
+      if (tid == 1023 && ncell == NMS_WG_CELLS) { s_cst[ncell] = wbase + incl; s_cur[ncell] = wbase + incl; }
+    }
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+      const float4 q = gb[i];
+      if (q.z > q.x && q.w > q.y)
+        items[atomicAdd(&s_cur[gr_cell(0.5f * (q.y + q.w), g.oy, g.invy, g.gy) * g.gx +
+                               gr_cell(0.5f * (q.x + q.z), g.ox, g.invx, g.gx)], 1)] = i;
+    }
+    __syncthreads();
+    for (;;) {
+      const int cut0 = s_cut;
+      uint32_t word = 0u;
+      if (tid < nwords) {
+        word = s_alive[tid];
+        const int lo = cut0 + 1;
+        if ((tid + 1) * 32 <= lo) word = 0u;
+        else if (tid * 32 < lo) word &= ~0u << (lo - tid * 32);
+      }
+      const int pc = __popc(word);
+      int incl = pc;
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        const int v = __shfl_up(incl, o);
+        if (lane >= o) incl += v;
+      }
+      if (lane == 63) s_wsum[wave] = incl;
+      __syncthreads();
+      int wb = 0, tot = 0;
+      for (int w = 0; w < 16; ++w) { if (w < wave) wb += s_wsum[w]; tot += s_wsum[w]; }
+      const int m = min(64, tot);
+      if (m == 0) break;                              // block-uniform
+      {
+        int pos = wb + incl - pc;
+        uint32_t wv = word;
+        while (wv && pos < 64) {
+          const int bit = __ffs(wv) - 1;
+          wv &= wv - 1u;
+          s_win[pos] = tid * 32 + bit;
+          s_wb[pos] = gb[tid * 32 + bit];
+          ++pos;
+        }
+      }
+      __syncthreads();
+      for (int t = wave; t < m; t += 16) {
+        const float4 bt = s_wb[t];
+        const bool hit = lane > t && lane < m && iou_gt_f(bt, s_wb[lane < m ? lane : 0], thr_f, false);
+        const unsigned long long row = __ballot(hit);
+        if (lane == 0) s_wm[t] = row;
+      }
+      __syncthreads();
+      if (wave == 0) {
+        const int i = lane < m ? s_win[lane] : 0;
+        const unsigned long long rowl = lane < m ? s_wm[lane] : 0ull;
+        unsigned long long alive = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+        for (int t = 0; t < m; ++t) {
+          const unsigned long long rt = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(rowl >> 32), t) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowl, t);
+          if ((alive >> t) & 1ull) alive &= ~rt;
+        }
+        const bool kp = (alive >> lane) & 1ull;
+        const int pos = __popcll(alive & ((1ull << lane) - 1ull));
+        const int nk = s_nk;
+        if (kp) {
+          kept[nk + pos] = i;
+          s_wk[pos] = lane;                             // window slot (its box is in s_wb)
+        }
+        if (lane == 0) {
+          s_nk = nk + __popcll(alive);
+          s_nwk = __popcll(alive);
+          s_cut = s_win[m - 1];
+        }
+      }
+      __syncthreads();
+      const int nwk = s_nwk, cut = s_cut;
+      for (int k = wave; k < nwk; k += 16) {
+        const float4 bu = s_wb[s_wk[k]];
+        if (!(bu.z > bu.x && bu.w > bu.y)) continue;      // wave-uniform
+        int x0, x1, y0, y1;
+        gr_region(g, bu, tr, x0, x1, y0, y1);
+        for (int cy = y0; cy <= y1; ++cy) {
+          const int plo = s_cst[cy * g.gx + x0], phi = s_cst[cy * g.gx + x1 + 1];
+          for (int p = plo + lane; p < phi; p += 64) {
+            const int j = items[p];
+            if (j > cut && ((s_alive[j >> 5] >> (j & 31)) & 1u) && iou_gt_f(bu, gb[j], thr_f, false))
+              atomicAnd(&s_alive[j >> 5], ~(1u << (j & 31)));
+          }
+        }
+      }
+      __syncthreads();
+    }
+    // keep list -> anchor ids: kept[e] = idx[kept[e]] (each element by its own thread), then copy
+    const int nk = s_nk;
+    for (int e = tid; e < nk; e += 1024) kept[e] = idx[kept[e]];
+    __syncthreads();
+    for (int e = tid; e < nk; e += 1024) idx[e] = kept[e];
+    if (tid == 0) {
+      ws.cls_cnt[(long)b * nc + c] = nk;
+      ws.route[(long)b * nc + c] = 2;
+    }
+    __syncthreads();
+  }
 }
 
 __global__ void nms_compact_kernel(int A, int nc, NmsWs ws, int64_t* keep_idx, int* keep_lbl,
@@ -1859,30 +2097,15 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
   // kernel (level segments 0.358 -> 0.283 ms per B=32 call, profiles/r04w_*)
   int cap = 256;
   if (const char* e = getenv("YMS_NMS_CAP")) cap = std::min(NMS_CAP, std::max(1, atoi(e)));
-  hipLaunchKernelGGL(nms_bucket_kernel, dim3((unsigned)n), dim3(1024), (size_t)nc * 12, st, A, nc, score, label,
-                     boxes_xyxy, gmin, cap, w);
+  hipLaunchKernelGGL(nms_bucket_kernel, dim3((unsigned)n), dim3(1024), (size_t)nc * 8, st, A, nc, score, label,
+                     gmin, cap, w);
   hipLaunchKernelGGL(nms_class_kernel, dim3((unsigned)nc, (unsigned)n), dim3(256), 0, st, A, nc, boxes_xyxy, iou, cap,
                      w);
-  static bool gattr_set = false;
-  if (!gattr_set) {
-    if (hipFuncSetAttribute((const void*)nms_graph_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            NMS_GR_MAXN * 12) != hipSuccess)
-      return YMS_ERR_LAUNCH;
-    gattr_set = true;
-  }
-  const bool graph = gmin > 0 && A >= gmin;
-  if (graph) {
-    // the search radius' threshold, a little below thr_f (slack for the rounding of the bound)
-    const float tr = std::max(0.0f, thr_f * (1.0f - 1e-4f) - 1e-6f);
-    const unsigned segs = (unsigned)std::min(512, n * nc);
-    hipLaunchKernelGGL(nms_graph_build_kernel, dim3(segs), dim3(1024), 0, st, A, nc, boxes_xyxy, tr, maxc, w);
-    hipLaunchKernelGGL(nms_graph_pairs_kernel, dim3(2048), dim3(256), 0, st, A, nc, thr_f, tr, w);
-    hipLaunchKernelGGL(nms_graph_resolve_kernel, dim3(segs), dim3(1024), (size_t)NMS_GR_MAXN * 12, st, A, nc,
-                       thr_f, tr, w);
-  }
   static bool attr_set = false;
   if (!attr_set) {
-    if (hipFuncSetAttribute((const void*)nms_big_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+    if (hipFuncSetAttribute((const void*)nms_graph_resolve_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                            NMS_GR_MAXN * 12) != hipSuccess ||
+        hipFuncSetAttribute((const void*)nms_big_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             NMS_CHUNK * 8) != hipSuccess ||
         hipFuncSetAttribute((const void*)nms_chunk_sort_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             NMS_CHUNK * 8) != hipSuccess ||
@@ -1895,9 +2118,29 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
       return YMS_ERR_LAUNCH;
     attr_set = true;
   }
-  if (A > cap || graph) {           // (the graph build routes dense segments of any size here)
+  const bool graph = gmin > 0 && A >= gmin;
+  if (A > cap || graph) {            // big-path segments exist only then (bucket: route 3)
     const int full = iou < 0.0 ? 1 : 0;
     const unsigned segs = (unsigned)std::min(256, n * nc);
+    // the search radius' threshold, a little below thr_f (slack for the rounding of the bound)
+    const float tr = std::max(0.0f, thr_f * (1.0f - 1e-4f) - 1e-6f);
+    // 1. route + sort + window-grid greedy in one block per segment (finite segments of <= 8192
+    //    boxes): graph candidates go to the graph list, <= NMS_WG_MAX boxes are resolved here
+    //    (YMS_NMS_WGRID=0: routing only); the rest stay for the kernels below (route 3)
+    const char* genv = getenv("YMS_NMS_WGRID");
+    const int wg_on = (genv && atoi(genv) == 0) ? 0 : 1;
+    if (!full && (wg_on || graph))
+      hipLaunchKernelGGL(nms_wgrid_kernel, dim3(segs), dim3(1024), NMS_WG_LDS, st, A, nc, boxes_xyxy, thr_f, tr,
+                         gmin, maxc, wg_on, w);
+    // 2. graph kernels on the graph list
+    if (graph && !full) {
+      const unsigned gsegs = (unsigned)std::min(512, n * nc);
+      hipLaunchKernelGGL(nms_graph_build_kernel, dim3(gsegs), dim3(1024), 0, st, A, nc, boxes_xyxy, tr, w);
+      hipLaunchKernelGGL(nms_graph_pairs_kernel, dim3(2048), dim3(256), 0, st, A, nc, thr_f, tr, w);
+      hipLaunchKernelGGL(nms_graph_resolve_kernel, dim3(gsegs), dim3(1024), (size_t)NMS_GR_MAXN * 12, st, A, nc,
+                         thr_f, tr, w);
+    }
+    // 3. the rest (route 3): sorted, then the kept-list greedy (or the opt-in window kernel)
     if (A > NMS_CHUNK)
       hipLaunchKernelGGL(nms_chunk_sort_kernel, dim3(256), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc, w);
     hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc,
@@ -1912,19 +2155,15 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     // per call).  Measured (profiles/r04c_nms_kernels.txt): 267 vs 343 us on the bench's level
     // segments (~115 kept of 6400), but 4.0 ms on uniform small boxes where most candidates are kept
     // (its test phase is candidates x kept boxes on one CU; the grid greedy prunes spatially).
-    // window-grid greedy for sorted segments of <= NMS_WG_MAX finite boxes (YMS_NMS_WGRID=0: off)
-    const char* genv = getenv("YMS_NMS_WGRID");
-    if (!full && !(genv && atoi(genv) == 0)) {
-      const float trg = std::max(0.0f, thr_f * (1.0f - 1e-4f) - 1e-6f);
-      hipLaunchKernelGGL(nms_wgrid_kernel, dim3(segs), dim3(1024), NMS_WG_LDS, st, A, nc, thr_f, trg, w);
-    }
     const char* wenv = getenv("YMS_NMS_WINDOW");
     const int win_max = (wenv && atoi(wenv) == 1) ? NMS_WIN_MAX : 0;
+    // the window-grid greedy over global memory for sorted finite segments of NMS_WG_MAX..NMS_WGG_MAX
+    if (!full && wg_on && A > NMS_WG_MAX)
+      hipLaunchKernelGGL(nms_wgrid_glb_kernel, dim3(segs), dim3(1024), 0, st, A, nc, thr_f, tr, w);
     if (win_max > 0)
       hipLaunchKernelGGL(nms_window_kernel, dim3(segs), dim3(1024), NMS_WIN_LDS, st, A, nc, thr_f, full, w);
-    if (A > win_max)
-      hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
-                         thr_f, full, grid_min, win_max, w);
+    hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
+                       thr_f, full, grid_min, win_max, w);
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
