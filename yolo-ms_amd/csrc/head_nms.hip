@@ -121,9 +121,19 @@ __global__ __launch_bounds__(256) void nms_prep_kernel(int n, int A, int nc, con
     float best = -INFINITY;
     int bl = 0x7fffffff;
     bool any = false;
-    for (int c = sub; c < nc; c += 16) {
-      const float v = q[4 + c];
-      if (!any || v > best) { best = v; bl = c; any = true; }
+    // this lane's classes c = sub, sub + 16, ...: loads batched 8 deep (nc = 80: one batch)
+    for (int c0 = sub; c0 < nc; c0 += 128) {
+      float v8[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + 16 * u;
+        v8[u] = c < nc ? q[4 + c] : 0.0f;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int c = c0 + 16 * u;
+        if (c < nc && (!any || v8[u] > best)) { best = v8[u]; bl = c; any = true; }
+      }
     }
 #pragma unroll
     for (int off = 8; off > 0; off >>= 1) {
