@@ -331,8 +331,12 @@ yms_status yms_nms_prep(int n, int A, int nc, const float* pred, float conf, flo
                         float* score, int* label, void* stream);
 /* Class-wise NMS over the prep output.  keep_idx[n][A] (anchor ids), keep_lbl[n][A],
  * counts[n]; per image the kept rows are ordered by class ascending, then by descending
- * score (ties by anchor id), exactly like the reference's per-class torchvision loop. */
+ * score (ties by anchor id), exactly like the reference's per-class torchvision loop.
+ * ws: at least yms_nms_ws_bytes_min() bytes; with yms_nms_ws_bytes() bytes (+ ~530 B per anchor
+ * of suppressee lists) big sparse-overlap segments may also take the graph kernels.  Every routing
+ * gives the same keep lists. */
 size_t yms_nms_ws_bytes(int n, int A, int nc);
+size_t yms_nms_ws_bytes_min(int n, int A, int nc);
 yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, const float* score,
                              const int* label, double iou, int64_t* keep_idx, int* keep_lbl,
                              int* counts, void* ws, size_t ws_bytes, void* stream);

@@ -47,6 +47,9 @@ def test_host_shape_validation_and_sizes():
     assert L.lib().yms_conv_fwd(ctypes.pointer(bad), None, 8, 0, None, None, 8, 0, None, None, 0, None, 0, 0,
                                 None, None) == 1
     assert L.lib().yms_nms_ws_bytes(32, 8400, 80) > 32 * 8400 * 28
+    # without the graph kernels' suppressee lists: ~56 B per anchor instead of ~590
+    full, base = L.lib().yms_nms_ws_bytes(32, 8400, 80), L.lib().yms_nms_ws_bytes_min(32, 8400, 80)
+    assert 32 * 8400 * 40 < base < 32 * 8400 * 80 and full - base > 32 * 8400 * 512
 
 
 def test_bn_bwd_rows_is_the_launched_block_count():

@@ -45,3 +45,24 @@ def test_cpu_tensors_fail_loudly():
         assert "GPU" in str(e)
     else:
         raise AssertionError("CPU tensors must raise (no CPU fallback)")
+
+
+def test_bbox_iou_is_pairwise_like_torchvision():
+    """simplified_loss.py:170-185 returns torchvision's PAIRWISE [N, M] box_iou / complete_box_iou
+    (ADVICE r4: the elementwise loss.py helper gave [N] or a broadcast error).  Known answers;
+    parity with torchvision itself is unpinned (not installed)."""
+    b1 = torch.tensor([[5.0, 5.0, 10.0, 10.0], [20.0, 20.0, 4.0, 4.0], [5.0, 5.0, 2.0, 2.0]])   # xywh
+    b2 = torch.tensor([[5.0, 5.0, 10.0, 10.0], [10.0, 5.0, 10.0, 10.0]])
+    iou = S.bbox_iou(b1, b2)
+    assert iou.shape == (3, 2)
+    assert torch.allclose(iou[0], torch.tensor([1.0, 1.0 / 3.0]))      # identical; half-overlap 50/150
+    assert torch.all(iou[1] == 0)                                        # disjoint
+    assert torch.isclose(iou[2, 0], torch.tensor(4.0 / 100.0))          # contained 2x2 in 10x10
+    xyxy = S.bbox_iou(torch.tensor([[0.0, 0.0, 10.0, 10.0]]), torch.tensor([[0.0, 0.0, 10.0, 5.0]]), xywh=False)
+    assert xyxy.shape == (1, 1) and torch.isclose(xyxy[0, 0], torch.tensor(0.5))
+    ciou = S.bbox_iou(b1, b2, CIoU=True)
+    assert ciou.shape == (3, 2) and torch.isclose(ciou[0, 0], torch.tensor(1.0))
+    # CIoU <= IoU (centre-distance and aspect penalties are non-negative); equal aspect ratios leave
+    # only the centre term: (10-5)^2 / (15^2 + 10^2 + eps)
+    assert torch.all(ciou <= iou + 1e-6)
+    assert torch.isclose(ciou[0, 1], torch.tensor(1.0 / 3.0 - 25.0 / 325.0), atol=1e-6)

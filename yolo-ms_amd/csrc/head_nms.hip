@@ -1956,7 +1956,19 @@ __global__ void nms_compact_kernel(int A, int nc, NmsWs ws, int64_t* keep_idx, i
 }
 
 static size_t r256(size_t x) { return (x + 255) & ~(size_t)255; }
-static NmsWs carve(void* ws, int n, int A, int nc) {
+// Workspace layout: the arrays every routing uses first, then the graph kernels' scratch (suppressee
+// lists, ~530 B per anchor).  A workspace of only the first part (yms_nms_ws_bytes_min) runs every
+// segment on the other exact routes (window-grid / kept-list greedy), with identical results.
+static size_t ws_base_bytes(int n, int A, int nc) {
+  return r256((size_t)n * A * 8) + r256((size_t)n * A * 16) + r256((size_t)n * A * 4) + r256((size_t)n * nc * 4) +
+         r256((size_t)n * nc * 4) + r256((size_t)(1 + 2 * n * nc) * 4) + r256((size_t)(3 + 2 * n * nc) * 4) +
+         r256((size_t)n * nc * 4) + r256((size_t)n * A * 8) + r256((size_t)n * (A + nc) * 4);
+}
+static size_t ws_graph_bytes(int n, int A, int nc) {
+  return r256((size_t)n * A * NMS_GR_ROW * 2) + r256((size_t)n * A) + r256((size_t)n * A * 2) +
+         r256((size_t)n * nc * sizeof(GraphSeg)) + r256((size_t)2 * n * A * sizeof(int2));
+}
+static NmsWs carve(void* ws, int n, int A, int nc, bool graph) {
   char* p = (char*)ws;
   NmsWs w;
   w.gkeys = (uint64_t*)p;
@@ -1979,6 +1991,12 @@ static NmsWs carve(void* ws, int n, int A, int nc) {
   p += r256((size_t)n * A * 8);
   w.cellst = (int*)p;
   p += r256((size_t)n * (A + nc) * 4);
+  w.sup = nullptr;
+  w.scnt = nullptr;
+  w.indeg = nullptr;
+  w.gseg = nullptr;
+  w.gwork = nullptr;
+  if (!graph) return w;
   w.sup = (uint16_t*)p;
   p += r256((size_t)n * A * NMS_GR_ROW * 2);
   w.scnt = (uint8_t*)p;
@@ -2070,21 +2088,18 @@ yms_status yms_nms_prep(int n, int A, int nc, const float* pred, float conf, flo
   return launch_status();
 }
 
-size_t yms_nms_ws_bytes(int n, int A, int nc) {
-  return r256((size_t)n * A * 8) + r256((size_t)n * A * 16) + r256((size_t)n * A * 4) +
-         r256((size_t)n * nc * 4) + r256((size_t)n * nc * 4) + r256((size_t)(1 + 2 * n * nc) * 4) +
-         r256((size_t)(3 + 2 * n * nc) * 4) + r256((size_t)n * nc * 4) + r256((size_t)n * A * 8) +
-         r256((size_t)n * (A + nc) * 4) + r256((size_t)n * A * NMS_GR_ROW * 2) + r256((size_t)n * A) + r256((size_t)n * A * 2) +
-         r256((size_t)n * nc * sizeof(GraphSeg)) + r256((size_t)2 * n * A * sizeof(int2));
-}
+size_t yms_nms_ws_bytes(int n, int A, int nc) { return ws_base_bytes(n, A, nc) + ws_graph_bytes(n, A, nc); }
+size_t yms_nms_ws_bytes_min(int n, int A, int nc) { return ws_base_bytes(n, A, nc); }
 
 yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, const float* score,
                              const int* label, double iou, int64_t* keep_idx, int* keep_lbl,
                              int* counts, void* ws, size_t ws_bytes, void* stream) {
   if (n <= 0 || A <= 0 || nc <= 0 || !boxes_xyxy || !score || !keep_idx || !counts || !ws) return YMS_ERR_INVALID;
-  if (ws_bytes < yms_nms_ws_bytes(n, A, nc)) return YMS_ERR_INVALID;
+  if (ws_bytes < yms_nms_ws_bytes_min(n, A, nc)) return YMS_ERR_INVALID;
   if ((uintptr_t)ws % 16 != 0 || (uintptr_t)boxes_xyxy % 16 != 0) return YMS_ERR_INVALID;
-  NmsWs w = carve(ws, n, A, nc);
+  // the graph kernels' scratch is present only in a full-size workspace
+  const bool graph_ws = ws_bytes >= yms_nms_ws_bytes(n, A, nc);
+  NmsWs w = carve(ws, n, A, nc, graph_ws);
   hipStream_t st = (hipStream_t)stream;
   if (hipMemsetAsync(w.big, 0, (size_t)((char*)(w.gl + 2) - (char*)w.big), st) != hipSuccess) return YMS_ERR_LAUNCH;
   // float threshold with (float)x > thr_f  <=>  (double)x > iou  for every non-NaN float x
@@ -2099,7 +2114,7 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
   int gmin = 2048, maxc = 256;
   if (const char* e = getenv("YMS_NMS_GRAPH_MIN")) gmin = atoi(e);
   if (const char* e = getenv("YMS_NMS_GRAPH_MAXC")) maxc = atoi(e);   // 0: no density routing
-  if (iou < 0.0 || gmin < 0) gmin = 0;
+  if (iou < 0.0 || gmin < 0 || !graph_ws) gmin = 0;
   if (gmin > 0) gmin = std::max(gmin, 32);
   // segments above `cap` boxes go to the big-segment path (sort + window-grid / kept-list greedy);
   // YMS_NMS_CAP overrides (<= NMS_CAP, the class kernel's LDS capacity)

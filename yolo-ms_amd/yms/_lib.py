@@ -116,6 +116,7 @@ _SIGS = {
     "yms_dfl": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "yms_nms_prep": (_I, [_I, _I, _I, _P, _F, _P, _P, _P, _P]),
     "yms_nms_ws_bytes": (_SZ, [_I, _I, _I]),
+    "yms_nms_ws_bytes_min": (_SZ, [_I, _I, _I]),
     "yms_nms_classwise": (_I, [_I, _I, _I, _P, _P, _P, _D, _P, _P, _P, _P, _SZ, _P]),
     "yms_nms_single": (_I, [_I, _P, _P, _D, _P, _P, _P, _SZ, _P]),
 }

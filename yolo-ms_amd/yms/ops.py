@@ -4,6 +4,7 @@ standalone DFL integral.  GPU tensors only; every call goes through libyms.so.""
 from __future__ import annotations
 
 import ctypes
+import os
 
 import torch
 
@@ -28,6 +29,26 @@ def dfl(x, ch=16):
     return out
 
 
+_WS = {}
+
+
+def _nms_ws(dev, B, A, nc, iou):
+    """NMS scratch reused across calls on one stream (calls on a stream are ordered, so one buffer
+    per (device, stream) is safe; a call on another stream gets its own)."""
+    # graph NMS (csrc/head_nms.hip) runs on segments of at least YMS_NMS_GRAPH_MIN boxes (default
+    # 2048, 0 = off, at least 32, the C side's rule); without it the workspace leaves out the graph
+    # kernels' suppressee lists (~530 B per anchor) and every segment takes the other exact routes
+    gmin = int(os.environ.get("YMS_NMS_GRAPH_MIN", "2048"))
+    full = iou >= 0.0 and gmin > 0 and A >= max(gmin, 32)
+    nbytes = (L.lib().yms_nms_ws_bytes if full else L.lib().yms_nms_ws_bytes_min)(B, A, nc)
+    key = (dev.index, L.stream_ptr(dev))
+    ws = _WS.get(key)
+    if ws is None or ws.numel() < nbytes:
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        _WS[key] = ws
+    return ws, nbytes
+
+
 def nms(boxes, scores, iou_threshold):
     """torchvision.ops.nms(boxes [N,4] xyxy, scores [N], iou) -> int64 keep (score-descending)."""
     _cuda(boxes, scores)
@@ -39,8 +60,7 @@ def nms(boxes, scores, iou_threshold):
     s = scores.detach().float().contiguous()
     keep = torch.empty(n, dtype=torch.int64, device=dev)
     cnt = torch.empty(1, dtype=torch.int32, device=dev)
-    wsb = L.lib().yms_nms_ws_bytes(1, n, 1)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    ws, wsb = _nms_ws(dev, 1, n, 1, float(iou_threshold))
     L.call("yms_nms_single", n, b.data_ptr(), s.data_ptr(), ctypes.c_double(float(iou_threshold)),
            keep.data_ptr(), cnt.data_ptr(), ws.data_ptr(), wsb, L.stream_ptr(dev))
     return keep[:int(cnt.item())]
@@ -67,8 +87,7 @@ def batched_nms_indices(pred, conf_thresh=0.25, iou_thresh=0.45):
     keep = torch.empty((B, A), dtype=torch.int64, device=dev)
     klbl = torch.empty((B, A), dtype=torch.int32, device=dev)
     counts = torch.empty(B, dtype=torch.int32, device=dev)
-    wsb = L.lib().yms_nms_ws_bytes(B, A, nc)
-    ws = torch.empty(wsb, dtype=torch.uint8, device=dev)
+    ws, wsb = _nms_ws(dev, B, A, nc, float(iou_thresh))
     L.call("yms_nms_classwise", B, A, nc, bxy.data_ptr(), score.data_ptr(), label.data_ptr(),
            ctypes.c_double(float(iou_thresh)), keep.data_ptr(), klbl.data_ptr(), counts.data_ptr(),
            ws.data_ptr(), wsb, st)

@@ -91,6 +91,22 @@ class Layout:
         return off
 
 
+def _overlap(a, b):
+    return a.buf is b.buf and a.off < b.off + b.c and b.off < a.off + a.c
+
+
+def _check_not_in_place(op, y):
+    """GradTracker.release(y) clears y's gradient interval once its producer has taken it, so an
+    earlier writer of that memory stores instead of accumulating.  That is only sound when no
+    input of the same op lives in y's channels (an in-place op would lose its input's gradient):
+    every op's inputs are checked here."""
+    for name, v in vars(op).items() if hasattr(op, "__dict__") else ():
+        vs = v if isinstance(v, (list, tuple)) else (v,)
+        for u in vs:
+            if isinstance(u, View) and u is not y and name != "y" and _overlap(u, y):
+                raise RuntimeError(f"yms: {type(op).__name__}.{name} overlaps its output (in-place op)")
+
+
 class GradTracker:
     """Backward-order simulation deciding, for every write into an activation-gradient slice,
     whether it is the first one (plain store) or must accumulate; buffers that are read
@@ -777,6 +793,7 @@ class Plan:
                 op.plan_grads(T)
                 y = getattr(op, "y", None)
                 if isinstance(y, View) and not any(y is o for o in self.outputs):
+                    _check_not_in_place(op, y)
                     T.release(y)
             for op in self.ops:
                 if getattr(op, "bnred", None) is not None and op.acc_x:

@@ -11,6 +11,8 @@ from __future__ import annotations
 
 import os
 
+import threading
+
 import torch
 
 from . import _lib as L
@@ -295,15 +297,21 @@ def run(module, inputs, grad_hook=None):
     stream = L.stream_ptr(dev)
     decode = isinstance(plan.kind, tuple) and plan.kind[0] == "decode"
     with torch.no_grad():
-        # a decode plan returns a fresh tensor, so its arena is internal: keep it per stream (the
-        # next call on that stream is ordered after this one) and skip re-zeroing the pad ranges
-        cached = getattr(plan, "_infer_arena", None) if decode else None
-        if cached is not None and cached[0] == stream and cached[1].device == dev:
-            arena = cached[1]
-        else:
+        # a decode plan returns a fresh tensor, so its arena is internal: keep it per (stream, host
+        # thread) -- the next call from that thread on that stream is ordered after this one, while
+        # two threads sharing a stream would interleave their launches -- and skip
+        # re-zeroing the pad ranges
+        arena = None
+        if decode:
+            cache = plan.__dict__.setdefault("_infer_arenas", {})
+            key = (stream, threading.get_ident())
+            arena = cache.get(key)
+            if arena is not None and arena.device != dev:
+                arena = None
+        if arena is None:
             arena = plan.new_arena(dev, stream)
             if decode:
-                plan._infer_arena = (stream, arena)
+                cache[key] = arena
         rt = Rt(plan, arena.data_ptr(), stream, False)
         rt.eval_base = plan.ensure_eval_cache(dev, stream)
         _load_inputs(plan, rt, inputs)

@@ -24,9 +24,12 @@ produce d(loss)/d(head maps) with the value, so ``loss.backward()`` drives the p
 """
 from __future__ import annotations
 
+import math
+
+import torch
 from torch import nn
 
-from yolov8.tools.loss import ComputeLoss as _FusedComputeLoss, bbox_iou  # noqa: F401  (bbox_iou: train.py:14)
+from yolov8.tools.loss import ComputeLoss as _FusedComputeLoss
 
 __all__ = ["SimplifiedYOLOLoss", "ComputeLoss", "bbox_iou"]
 
@@ -65,3 +68,44 @@ def ComputeLoss(model_head=None, num_classes=80, device='cpu', img_size=(640, 64
     """The factory simplified_loss.py:156-167 keeps for backwards compatibility: returns a
     ``SimplifiedYOLOLoss`` over ``num_classes`` / ``img_size`` / ``strides``."""
     return SimplifiedYOLOLoss(num_classes=num_classes, device=device, img_size=img_size, strides=strides)
+
+
+def _pairwise_iou(b1, b2):
+    """[N,4] x [M,4] xyxy -> (iou [N,M], union [N,M]), torchvision ``box_iou``'s arithmetic."""
+    a1 = (b1[:, 2] - b1[:, 0]) * (b1[:, 3] - b1[:, 1])
+    a2 = (b2[:, 2] - b2[:, 0]) * (b2[:, 3] - b2[:, 1])
+    lt = torch.max(b1[:, None, :2], b2[None, :, :2])
+    rb = torch.min(b1[:, None, 2:], b2[None, :, 2:])
+    wh = (rb - lt).clamp(min=0)
+    inter = wh[..., 0] * wh[..., 1]
+    union = a1[:, None] + a2[None, :] - inter
+    return inter / union, union
+
+
+def bbox_iou(box1, box2, xywh=True, GIoU=False, DIoU=False, CIoU=False, eps=1e-7):
+    """The validation helper simplified_loss.py:170-185 defines (imported by train.py:14): the
+    PAIRWISE [N, M] IoU matrix of box1 [N,4] and box2 [M,4] -- torchvision ``box_iou``, or
+    ``complete_box_iou`` (eps 1e-7) when CIoU -- restated in torch ops on the boxes' device
+    (torchvision is absent here: parity with it is unpinned; tests/test_simplified_loss_cpu.py).
+    GIoU / DIoU are accepted and, as in the reference, ignored."""
+    if xywh:
+        box1 = torch.cat((box1[..., :2] - box1[..., 2:] / 2, box1[..., :2] + box1[..., 2:] / 2), dim=-1)
+        box2 = torch.cat((box2[..., :2] - box2[..., 2:] / 2, box2[..., :2] + box2[..., 2:] / 2), dim=-1)
+    iou, _ = _pairwise_iou(box1, box2)
+    if not CIoU:
+        return iou
+    # torchvision complete_box_iou: DIoU term over the enclosing box diagonal, then the aspect term
+    lti = torch.min(box1[:, None, :2], box2[None, :, :2])
+    rbi = torch.max(box1[:, None, 2:], box2[None, :, 2:])
+    whi = (rbi - lti).clamp(min=0)
+    diag = whi[..., 0] ** 2 + whi[..., 1] ** 2 + eps
+    c1 = (box1[:, :2] + box1[:, 2:]) / 2
+    c2 = (box2[:, :2] + box2[:, 2:]) / 2
+    cdist = ((c1[:, None, :] - c2[None, :, :]) ** 2).sum(-1)
+    diou = iou - cdist / diag
+    w1, h1 = box1[:, 2] - box1[:, 0], box1[:, 3] - box1[:, 1]
+    w2, h2 = box2[:, 2] - box2[:, 0], box2[:, 3] - box2[:, 1]
+    v = (4 / (math.pi ** 2)) * (torch.atan(w1 / h1)[:, None] - torch.atan(w2 / h2)[None, :]) ** 2
+    with torch.no_grad():
+        alpha = v / (1 - iou + v + eps)
+    return diou - alpha * v
