@@ -6,7 +6,7 @@ NAME=$1; DEFS=$2
 B=$R/tools/bin/build_$NAME
 mkdir -p $B
 cd $R/yolo-ms_amd/csrc
-for f in conv_igemm conv_halo wgrad_halo stem dwconv map_eval bn_pool head_nms det_loss preprocess; do
+for f in conv_igemm conv_direct wgrad_halo wgrad_ring stem dwconv map_eval bn_pool head_nms det_loss preprocess; do
   /opt/rocm/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -fPIC -munsafe-fp-atomics $DEFS -c $f.hip -o $B/$f.o &
 done
 wait

@@ -1,5 +1,5 @@
-// Device helpers shared by the implicit-GEMM convolution kernels (conv_igemm.hip) and the
-// halo-tiled 3x3 kernel (conv_halo.hip): MFMA wrappers, counted vmcnt waits, the raw barrier,
+// Device helpers shared by the convolution kernels (conv_igemm.hip, conv_direct.hip, stem.hip,
+// wgrad_*.hip, dwconv.hip): MFMA wrappers, counted vmcnt waits, the raw barrier,
 // raw-buffer LDS-DMA and the XCD-aware block remap.
 #pragma once
 #include "yms_common.hpp"

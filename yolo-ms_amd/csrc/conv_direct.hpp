@@ -1,0 +1,28 @@
+// Host interface of the direct 3x3 convolution for small channel counts (conv_direct.hip),
+// dispatched from yms_conv_fwd / yms_conv_dgrad / yms_conv_stats_rows in conv_igemm.hip.
+#pragma once
+#include "yms_common.hpp"
+
+namespace yms {
+
+struct DirectGeo {
+  int TW, TH;            // output tile (TW divides the map width)
+  int CP;                // 16-B chunks of reduction channels per pixel (4 or 8)
+  int NCF;               // 32-column MFMA fragments of output channels (1 or 2)
+  int tiles_x, tiles_y;
+  long ntiles;
+  int grid;              // persistent blocks (= statistics rows of a training forward)
+};
+
+// True when the direct kernel runs this conv: 16-bit, 3x3, stride 1, pad 1, reduction channels
+// rounded to 8 of 32 or 64, at most 64 output channels (a multiple of 8), map width a multiple of
+// 16.  mode 0 = forward (reduction = cin), 1 = stride-1 input gradient (reduction = cout).
+// YMS_DIRECT=0 turns it off (A/B and tests; read per call).
+bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g);
+
+yms_status conv_direct_launch(const yms_conv_shape* s, int mode, const DirectGeo& g, const void* src, int src_ld,
+                              int src_off, const void* wpacked, void* dst, int dst_ld, int dst_off,
+                              const float* scale, const float* shift, int act, const void* res, int res_ld,
+                              int res_off, float* stats, int accumulate, hipStream_t st);
+
+}  // namespace yms

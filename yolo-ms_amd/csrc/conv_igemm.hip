@@ -17,7 +17,7 @@
 // operands get 8 consecutive pixels per lane.  wgrad is split over pixels into fp32
 // partial slabs that a second kernel reduces deterministically (no atomics).
 #include "conv_common.hpp"
-#include "conv_halo.hpp"
+#include "conv_direct.hpp"
 #include "wgrad_halo.hpp"
 #include "wgrad_ring.hpp"
 
@@ -1644,6 +1644,8 @@ yms_status yms_conv_pack_weight(const yms_conv_shape* s, const float* w, void* p
 
 int yms_conv_stats_rows(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
+  DirectGeo dg;
+  if (conv_direct_geometry(s, 0, &dg)) return dg.grid;   // conv_direct_kernel: one row per block
   const long M = (long)s->n * s->ho * s->wo;
   if (s->dtype == YMS_F32) return (int)cdiv(M, 128);     // conv_nt_kernel: one row per 128-row tile
   const NtpGeo g = ntp_geo(choose_tile(s->cout).cfg);    // conv_ntp_kernel: one slot per block
@@ -1663,11 +1665,12 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   if (!view_ok(x_ld, x_off, s->cin) || !view_ok(y_ld, y_off, s->cout)) return YMS_ERR_INVALID;
   if (res && !view_ok(res_ld, res_off, s->cout)) return YMS_ERR_INVALID;
   const int es = elem_size(s->dtype);
-  if (!stats) {   // statistics rows come from the NT kernels only
-    HaloGeo hg;
-    if (conv_halo_geometry(s, 0, &hg))
-      return conv_halo_launch(s, 0, hg, x, x_ld, x_off, wpacked, y, y_ld, y_off, scale, shift, act, res, res_ld,
-                              res_off, stats, 0, (hipStream_t)stream);
+  {
+    // small-channel 3x3: the direct kernel (conv_direct.hip), statistics included
+    DirectGeo dg;
+    if (conv_direct_geometry(s, 0, &dg))
+      return conv_direct_launch(s, 0, dg, x, x_ld, x_off, wpacked, y, y_ld, y_off, scale, shift, act, res, res_ld,
+                                res_off, stats, 0, (hipStream_t)stream);
   }
   PackGeo g = pack_geo(s, 0);
   NTParams p{};
@@ -1736,7 +1739,8 @@ yms_status yms_conv_fwd_pro(const yms_conv_shape* s, const void* z, int z_ld, in
 }
 
 int yms_conv_fwd_pro_supported(const yms_conv_shape* s) {
-  return shape_ok(s) && s->dtype != YMS_F32 && s->stride == 1 && s->pad == s->k / 2 && s->cin <= NTP_PRO_MAX_C &&
+  // 1x1 consumers only (3x3 consumers measured +1.7 ms per step: profiles/r04c_pro_ab.txt)
+  return shape_ok(s) && s->k == 1 && s->dtype != YMS_F32 && s->stride == 1 && s->pad == 0 && s->cin <= NTP_PRO_MAX_C &&
          s->cin % 8 == 0 && s->ho == s->h && s->wo == s->w;
 }
 
@@ -1746,10 +1750,10 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
   if (!shape_ok(s) || !dz || !wpacked_t || !dx) return YMS_ERR_INVALID;
   if (!view_ok(dz_ld, dz_off, s->cout) || !view_ok(dx_ld, dx_off, s->cin)) return YMS_ERR_INVALID;
   {
-    HaloGeo hg;
-    if (conv_halo_geometry(s, 1, &hg))
-      return conv_halo_launch(s, 1, hg, dz, dz_ld, dz_off, wpacked_t, dx, dx_ld, dx_off, nullptr, nullptr, 0,
-                              nullptr, 0, 0, nullptr, accumulate, (hipStream_t)stream);
+    DirectGeo dg;
+    if (conv_direct_geometry(s, 1, &dg))
+      return conv_direct_launch(s, 1, dg, dz, dz_ld, dz_off, wpacked_t, dx, dx_ld, dx_off, nullptr, nullptr, 0,
+                                nullptr, 0, 0, nullptr, accumulate, (hipStream_t)stream);
   }
   NTParams p{};
   p.src = (const char*)dz;
