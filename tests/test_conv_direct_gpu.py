@@ -180,3 +180,61 @@ def test_direct_matches_implicit_gemm_bench_shapes(shp, monkeypatch):
         assert err <= 8e-3 * b.abs().max().item(), err
     assert torch.allclose(m1, m0, rtol=1e-5, atol=1e-6 * m0.abs().max().item())
     assert torch.allclose(v1, v0, rtol=1e-4)
+
+
+# stride-2 input gradient by parity class: (n, cin = dgrad outputs, h, w, cout = reduction); class
+# grids ceil(w/2) of 32 / 16, odd h / w (the last class row / column masked), cin of 8..64
+S2 = [
+    (2, 32, 64, 64, 64),
+    (1, 32, 40, 64, 64),
+    (2, 16, 32, 32, 32),
+    (2, 64, 30, 64, 64),
+    (1, 24, 33, 63, 64),
+    (3, 8, 18, 31, 32),
+]
+
+
+@pytest.mark.parametrize("dt", ["bf16", "f16"])
+@pytest.mark.parametrize("shp", S2)
+def test_direct_dgrad_stride2(shp, dt):
+    n, cin, h, w, cout = shp
+    dtype = DT[dt]
+    g = torch.Generator().manual_seed(13 + sum(shp))
+    wt = torch.randn(cout, cin, 3, 3, generator=g) / (cout * 9) ** 0.5
+    sh = shape(n, h, w, cin, cout, 3, 2, dtype)
+    dz = torch.randn(n, cout, sh.ho, sh.wo, generator=g)
+    sp = ctypes.pointer(sh)
+    xr = torch.zeros(n, cin, h, w, requires_grad=True)
+    F.conv2d(xr, wt.to(dtype).float(), None, 2, 1).backward(dz.to(dtype).float())
+    wpt = pack(wt, sh, dtype, 1)
+    dzb = nhwc(dz, dtype)
+    for acc in (0, 1):
+        base = torch.randn(n, cin, h, w, generator=g) if acc else torch.zeros(n, cin, h, w)
+        dx = nhwc(base, dtype, ld=r8(cin) + 8)           # a wider buffer: channel slice of it
+        L.call("yms_conv_dgrad", sp, dzb.data_ptr(), dzb.shape[-1], 0, wpt.data_ptr(), dx.data_ptr(),
+               dx.shape[-1], 0, acc, L.stream_ptr())
+        exp = xr.grad + (base.to(dtype).float() if acc else 0)
+        _close(nchw(dx, cin).cpu(), exp, TOL[dt] * (2 if acc else 1))
+        assert dx[..., r8(cin):].abs().max().item() == 0
+
+
+def test_direct_dgrad_stride2_bench_shape(monkeypatch):
+    """The 320^2 32->64 stride-2 layer of the S@640 backbone: direct kernel vs the implicit GEMM's
+    parity-class path (YMS_DIRECT=0) on the same operands."""
+    n, cin, h, w, cout = 16, 32, 320, 320, 64
+    dtype = torch.bfloat16
+    g = torch.Generator(device="cuda").manual_seed(6)
+    wt = torch.randn(cout, cin, 3, 3, device="cuda", generator=g) / (cout * 9) ** 0.5
+    sh = shape(n, h, w, cin, cout, 3, 2, dtype)
+    dz = torch.randn(n, sh.ho, sh.wo, cout, device="cuda", generator=g).to(dtype)
+    sp = ctypes.pointer(sh)
+    wpt = pack(wt, sh, dtype, 1)
+    outs = []
+    for mode in ("1", "0"):
+        monkeypatch.setenv("YMS_DIRECT", mode)
+        dx = torch.empty(n, h, w, cin, dtype=dtype, device="cuda")
+        L.call("yms_conv_dgrad", sp, dz.data_ptr(), cout, 0, wpt.data_ptr(), dx.data_ptr(), cin, 0, 0,
+               L.stream_ptr())
+        outs.append(dx.float())
+    err = (outs[0] - outs[1]).abs().max().item()
+    assert err <= 8e-3 * outs[1].abs().max().item(), err

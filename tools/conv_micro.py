@@ -35,7 +35,7 @@ if os.environ.get("YMS_MICRO_SHAPES") == "wg":   # every distinct 3x3 layer of Y
               (64, 40, 40, 256, 80, 3, 1), (64, 20, 20, 512, 64, 3, 1), (64, 20, 20, 512, 80, 3, 1)]
 if os.environ.get("YMS_MICRO_SHAPES") == "direct":   # the direct small-channel 3x3 kernel's layers
     SHAPES = [(64, 80, 80, 64, 64, 3, 1), (64, 160, 160, 32, 32, 3, 1), (8, 320, 320, 32, 32, 3, 1),
-              (8, 160, 160, 64, 64, 3, 1)]
+              (8, 160, 160, 64, 64, 3, 1), (64, 320, 320, 32, 64, 3, 2)]
 dt = torch.bfloat16
 st = L.stream_ptr()
 

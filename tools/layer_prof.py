@@ -75,3 +75,22 @@ for n, k, t, fl in rows:
 print("per layer shape (count, total us, TF/s):")
 for (n, k), (c, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:45]:
     print(f"{n:28s} {k:34s} x{c:2d} {t * 1e3:9.1f} us {fl / (t * 1e-3) / 1e12 if fl else 0:7.1f} TF/s")
+# every fwd / dgrad layer shape with its own roofline: max(FLOPs / 2.5 PF, bytes / 8 TB/s), bytes =
+# input + output (16-bit) + weights once
+if os.environ.get("YMS_LAYER_ALL"):
+    print("fwd / dgrad per layer shape: calls, us per call, roofline us, frac")
+    tot_t = tot_r = 0.0
+    for (n, k), (c, t, fl) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        if n not in ("yms_conv_fwd", "yms_conv_dgrad"):
+            continue
+        nn, io, ks = k.split()
+        bb, hh, ww = (int(v) for v in nn.split("x"))
+        ci, co = (int(v) for v in io.split("->"))
+        kk, ss = int(ks[1]), int(ks[3])
+        ho, wo = (hh + 2 * (kk // 2) - kk) // ss + 1, (ww + 2 * (kk // 2) - kk) // ss + 1
+        byt = 2 * (bb * hh * ww * ci + bb * ho * wo * co + ci * co * kk * kk)
+        roof = max(fl / c / 2.5e15, byt / 8e12) * 1e6
+        tot_t += t * 1e3
+        tot_r += roof * c
+        print(f"{n:16s} {k:34s} x{c:2d} {t * 1e3 / c:8.1f} us  roof {roof:6.1f} us  frac {roof * c / (t * 1e3):.2f}")
+    print(f"total {tot_t:.1f} us, roofline {tot_r:.1f} us, frac {tot_r / tot_t:.3f}")

@@ -25,6 +25,7 @@
 // Input gradient (stride 1, pad 1): dx(y, x) = sum_t dz(y + 1 - dy_t, x + 1 - dx_t) W_t^T, i.e. the
 // same halo with the taps mirrored and the transposed packing of yms_conv_pack_weight(for_dgrad=1).
 #include <algorithm>
+#include <type_traits>
 #include <cstdlib>
 
 #include "conv_common.hpp"
@@ -50,10 +51,12 @@ struct DirectParams {
   float* stats;
   int stats_ld;
   float* stats_cnt;
-  int H, W;                    // map (stride 1: source = output)
+  int H, W;                    // source map (stride 1: also the output map)
+  int OH, OW;                  // output map
   int tiles_x, tiles_y, ntiles;
   int Ncols;                   // valid output channels (multiple of 8)
   int nkt;                     // packed weight k-tiles per row (row pitch nkt * 128 B)
+  int wrows;                   // packed weight rows (128-padded): the stride-2 class blocks' pitch
   uint32_t src_bytes, dst_bytes, res_bytes;
 };
 
@@ -447,32 +450,272 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
 }
 
 // ------------------------------------------------------------------------------------------
+// Stride-2 input gradient (pad 1, k 3) by output parity class, for the same channel range.  For
+// dx pixel (2a + ry, 2b + rx) only the taps kh = kh0 + 2jy, kw = kw0 + 2jx contribute (kh0 = 1 - ry,
+// jy < 1 + ry; likewise for x), reading dz(a + ry - jy, b + rx - jx): tiles of 256 class positions
+// (a, b) need one (TH+1) x (TW+1) halo of dz, and the four classes (1, 2, 2, 4 taps: 9 in all, the
+// stride-1 kernel's MFMA work per 256 positions) run one after the other on it, each writing its
+// 256 dx pixels.  Weights: the parity-class packing of yms_conv_pack_weight(for_dgrad=1, stride 2).
+// ------------------------------------------------------------------------------------------
+template <int TW, int CP, int NCF> struct DirGeo2 {
+  static constexpr int NTHR = 512, NW = 8, BM = 256, TH = BM / TW;
+  static constexpr int HWD = TW + 1, HP = (TH + 1) * HWD;
+  static constexpr int PITCH = CP * 16, HGR = HP * CP, NP = (HGR + NTHR - 1) / NTHR;
+  static constexpr int COP = 32 * NCF;
+  static constexpr int taps(int c) { return (1 + (c >> 1)) * (1 + (c & 1)); }
+  static constexpr int nkt(int c) { return (taps(c) * CP + 7) / 8; }
+  static constexpr int cumk(int c) { return c == 0 ? 0 : cumk(c - 1) + nkt(c - 1); }
+  static constexpr int NKT = cumk(4);
+  static constexpr int WBYTES = NKT * COP * 128;
+  static constexpr int BUF = HP * PITCH;
+  static constexpr int LDS = WBYTES + 2 * BUF;
+  static constexpr int OCC = LDS <= 80 * 1024 ? 2 : 1;
+  static constexpr int SS = CP == 8 ? 1 : 2;
+  static constexpr int NST = 2 * NCF;                  // 16-B stores per lane per class
+  static_assert((CP == 4 || CP == 8) && BM % TW == 0 && LDS <= 160 * 1024, "tile");
+};
+
+template <typename T, int TW, int CP, int NCF, int EPI>
+__global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_direct_dgrad2_kernel(DirectParams p) {
+  using G = DirGeo2<TW, CP, NCF>;
+  constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
+  constexpr int ES = (int)sizeof(T);
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  char* const wts = smem;
+  char* const bufs = smem + G::WBYTES;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+  const int wv = __builtin_amdgcn_readfirstlane(wave);
+  const int Gn = gridDim.x;
+  const int lb = xcd_remap(blockIdx.x, Gn);
+  if (lb >= p.ntiles) return;
+
+  const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)p.src_bytes, NT_RSRC3);
+  const __amdgpu_buffer_rsrc_t rs_dst = __builtin_amdgcn_make_buffer_rsrc((void*)p.dst, (short)0, (int)p.dst_bytes, NT_RSRC3);
+
+  // ---- resident weights: class blocks [kt][COP][128 B] (swizzled as in the stride-1 kernel) ----
+  {
+    const __amdgpu_buffer_rsrc_t rs_w = __builtin_amdgcn_make_buffer_rsrc((void*)p.wp, (short)0, 0x7fffffff, NT_RSRC3);
+    constexpr int WGR = G::NKT * COP * 8, WPASS = (WGR + NTHR - 1) / NTHR;
+#pragma unroll
+    for (int j = 0; j < WPASS; ++j) {
+      const int g = j * NTHR + tid;
+      if (WGR % NTHR == 0 || g < WGR) {
+        const int K = g / (COP * 8), r = (g >> 3) % COP, slot = g & 7;
+        const int c = K >= G::cumk(3) ? 3 : K >= G::cumk(2) ? 2 : K >= G::cumk(1) ? 1 : 0;
+        const int ktl = K - G::cumk(c);
+        const int nk = G::nkt(c);
+        const int ch = slot ^ ((r >> 1) & 7);
+        const long el = (long)p.wrows * 64 * G::cumk(c) + (long)r * nk * 64;
+        blds16(rs_w, wts + j * NTHR * 16 + wv * 1024, (uint32_t)(el * 2 + (ktl * 8 + ch) * 16));
+      }
+    }
+  }
+  auto tile_pos = [&](int t, int& n, int& tyi, int& txi) {
+    txi = t % p.tiles_x;
+    const int r = t / p.tiles_x;
+    tyi = r % p.tiles_y;
+    n = r / p.tiles_y;
+  };
+  // ---- dz halo rows a0 .. a0 + TH, columns b0 .. b0 + TW ----
+  int hl_hy[G::NP], hl_hx[G::NP], hl_c[G::NP];
+#pragma unroll
+  for (int j = 0; j < G::NP; ++j) {
+    const int g = j * NTHR + tid;
+    const int px = g / CP, slot = g % CP;
+    hl_hy[j] = px / HWD;
+    hl_hx[j] = px - (px / HWD) * HWD;
+    hl_c[j] = (slot ^ ((px >> G::SS) & (CP - 1))) * 16;
+  }
+  auto issue_halo = [&](int t, int b) {
+    int n, tyi, txi;
+    tile_pos(t, n, tyi, txi);
+    const int y0 = tyi * TH, x0 = txi * TW;
+    const int pix0 = (n * p.H + y0) * p.W + x0;      // p.H x p.W: the dz map
+    char* base = bufs + b * BUF + wv * 1024;
+#pragma unroll
+    for (int j = 0; j < G::NP; ++j) {
+      const int iy = y0 + hl_hy[j], ix = x0 + hl_hx[j];
+      const bool ok = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W;
+      const uint32_t vo =
+          ok ? (uint32_t)(((pix0 + hl_hy[j] * p.W + hl_hx[j]) * p.src_ld + p.src_off) * ES + hl_c[j]) : NT_OOB;
+      if (G::HGR % NTHR == 0 || j + 1 < G::NP || j * NTHR + tid < G::HGR)
+        if (YMS_DIRECT_DIAG != 5) blds16(rs_src, base + j * NTHR * 16, vo);
+    }
+  };
+  const int hr = wave * 32 + lr;
+  const int oty = hr / TW, otx = hr - (hr / TW) * TW;
+  // dx pixel (2a + ry, 2b + rx) of this lane's position, chunk (cf, pp)
+  auto out_off = [&](int n, int tyi, int txi, int cls, int cf, int pp, bool& ok) -> uint32_t {
+    const int oy = 2 * (tyi * TH + oty) + (cls >> 1), ox = 2 * (txi * TW + otx) + (cls & 1);
+    const int c0 = cf * 32 + 16 * pp + 8 * lh;
+    ok = oy < p.OH && ox < p.OW && c0 < p.Ncols;
+    return (uint32_t)((((n * p.OH + oy) * p.OW + ox) * p.dst_ld + p.dst_off + c0) * ES);
+  };
+  int bb[NCF];
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf) {
+    const int col = cf * 32 + lr;
+    bb[cf] = col * 128 + ((lh ^ ((col >> 1) & 7)) << 4);
+  }
+
+  const int my_tiles = (p.ntiles - lb + Gn - 1) / Gn;
+  constexpr bool ACC = EPI == EPI_ACCUM;
+  u32x4 rv[4][NCF][2];
+  auto load_ops = [&](int t) {
+    if constexpr (!ACC) return;
+    int n, tyi, txi;
+    tile_pos(t, n, tyi, txi);
+#pragma unroll
+    for (int c = 0; c < 4; ++c)
+#pragma unroll
+      for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+        for (int pp = 0; pp < 2; ++pp) {
+          bool ok;
+          const uint32_t o = out_off(n, tyi, txi, c, cf, pp, ok);
+          rv[c][cf][pp] = cd_ld16(rs_dst, ok ? o : NT_OOB);
+        }
+  };
+
+  f32x16 acc[NCF];
+  auto compute = [&](int b, auto cls_c) {
+    constexpr int c = decltype(cls_c)::value;
+    constexpr int ry = c >> 1, rx = c & 1, ntx = 1 + rx, taps = G::taps(c);
+    constexpr int KS = taps * CP / 2, KG = CP / 2, NG = KS / KG;
+    const char* Hb = bufs + b * BUF;
+    const char* Wc = wts + G::cumk(c) * COP * 128;
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) acc[cf][i] = 0.0f;
+    u32x4 af[2][KG], bf[2][KG][NCF];
+    auto frags = [&](int grp, int slot) {
+#pragma unroll
+      for (int j = 0; j < KG; ++j) {
+        const int ks = grp * KG + j, tl = ks / (CP / 2), kc = ks % (CP / 2);
+        const int jy = tl / ntx, jx = tl % ntx;
+        const int hp = (oty + ry - jy) * HWD + (otx + rx - jx);
+        const int ab = hp * PITCH + ((lh ^ ((hp >> G::SS) & (CP - 1))) << 4);
+        af[slot][j] = *reinterpret_cast<const u32x4*>(Hb + (ab ^ (kc << 5)));
+        const int q0 = tl * CP + 2 * kc, kt = q0 >> 3, cw0 = q0 & 7;
+#pragma unroll
+        for (int cf = 0; cf < NCF; ++cf)
+          bf[slot][j][cf] = *reinterpret_cast<const u32x4*>(Wc + kt * COP * 128 + (bb[cf] ^ (cw0 << 4)));
+      }
+    };
+    frags(0, 0);
+#pragma unroll
+    for (int grp = 0; grp < NG; ++grp) {
+      __builtin_amdgcn_sched_barrier(0);
+      if (grp + 1 < NG) frags(grp + 1, (grp + 1) & 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int j = 0; j < KG; ++j)
+#pragma unroll
+        for (int cf = 0; cf < NCF; ++cf) acc[cf] = Mfma<T>::mma(bf[grp & 1][j][cf], af[grp & 1][j], acc[cf]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  };
+  auto epilogue = [&](int t, int c) {
+    int n, tyi, txi;
+    tile_pos(t, n, tyi, txi);
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+      for (int pp = 0; pp < 2; ++pp) {
+        const int i0 = 8 * pp;
+        uint32_t a0 = cd_pack2<T>(acc[cf][i0], acc[cf][i0 + 1]), a1 = cd_pack2<T>(acc[cf][i0 + 2], acc[cf][i0 + 3]);
+        uint32_t b0 = cd_pack2<T>(acc[cf][i0 + 4], acc[cf][i0 + 5]), b1 = cd_pack2<T>(acc[cf][i0 + 6], acc[cf][i0 + 7]);
+        cd_swap(a0, b0);
+        cd_swap(a1, b1);
+        u32x4 ov = {a0, a1, b0, b1};
+        if constexpr (ACC) {
+          float f[8], r[8];
+          unpack8(*reinterpret_cast<const Raw8<T>*>(&ov), f);
+          unpack8(*reinterpret_cast<const Raw8<T>*>(&rv[c][cf][pp]), r);
+          ov = u32x4{cd_pack2<T>(f[0] + r[0], f[1] + r[1]), cd_pack2<T>(f[2] + r[2], f[3] + r[3]),
+                     cd_pack2<T>(f[4] + r[4], f[5] + r[5]), cd_pack2<T>(f[6] + r[6], f[7] + r[7])};
+        }
+        bool ok;
+        const uint32_t off = out_off(n, tyi, txi, c, cf, pp, ok);
+        cd_st16(rs_dst, ok ? off : NT_OOB, ov);
+      }
+  };
+
+  // vector-memory order per wave: prologue halo(lb) (drained), ops(lb), halo(lb + G); tile t:
+  // [barrier] halo(t + G), 4 x (compute, epilogue stores), ops(t + G)
+  issue_halo(lb, 0);
+  wait_vmcnt<0>();
+  __syncthreads();
+  load_ops(lb);
+  if (my_tiles > 1) issue_halo(lb + Gn, 1);
+  for (int it = 0, t = lb; it < my_tiles; ++it, t += Gn) {
+    const int b = it & 1;
+    const bool has_next = it + 1 < my_tiles;
+    if (it > 0) {
+      if (ACC) wait_vmcnt<(ACC ? 8 : 4) * G::NST>();    // younger: 4 classes' stores (+ ops(t))
+      else wait_vmcnt<4 * G::NST>();
+      __builtin_amdgcn_s_waitcnt((0xF) | (3 << 14) | (0x7 << 4) | (0 << 8));   // lgkmcnt(0)
+      raw_barrier();
+      if (has_next) issue_halo(t + Gn, b ^ 1);
+    }
+    compute(b, std::integral_constant<int, 0>{});
+    if constexpr (ACC) {
+      if (has_next) wait_vmcnt<G::NP - 1>();     // ops(t); halo(t + G) may stay in flight
+      else wait_vmcnt<0>();
+    }
+    epilogue(t, 0);
+    compute(b, std::integral_constant<int, 1>{});
+    epilogue(t, 1);
+    compute(b, std::integral_constant<int, 2>{});
+    epilogue(t, 2);
+    compute(b, std::integral_constant<int, 3>{});
+    epilogue(t, 3);
+    if (has_next) load_ops(t + Gn);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // host side
 // ------------------------------------------------------------------------------------------
+template <template <int, int, int> class GEO>
+static int direct_occ(int tw, int cp, int ncf) {
+  if (tw == 32) {
+    if (cp == 8) return ncf == 2 ? GEO<32, 8, 2>::OCC : GEO<32, 8, 1>::OCC;
+    return ncf == 2 ? GEO<32, 4, 2>::OCC : GEO<32, 4, 1>::OCC;
+  }
+  if (cp == 8) return ncf == 2 ? GEO<16, 8, 2>::OCC : GEO<16, 8, 1>::OCC;
+  return ncf == 2 ? GEO<16, 4, 2>::OCC : GEO<16, 4, 1>::OCC;   // (constants only: nothing launched)
+}
+
 bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g) {
   const char* e = getenv("YMS_DIRECT");
   if (e && atoi(e) == 0) return false;
-  if (!s || s->dtype == YMS_F32 || s->k != 3 || s->stride != 1 || s->pad != 1) return false;
-  if (s->ho != s->h || s->wo != s->w) return false;
+  if (!s || s->dtype == YMS_F32 || s->k != 3 || s->pad != 1) return false;
+  const bool s2 = s->stride == 2;
+  if (s2 ? (mode != 1 || s->ho != (s->h + 1) / 2 || s->wo != (s->w + 1) / 2)
+         : (s->stride != 1 || s->ho != s->h || s->wo != s->w))
+    return false;
   const int cr = mode == 0 ? s->cin : s->cout;      // reduction channels
   const int co = mode == 0 ? s->cout : s->cin;      // output channels
   const int cr8 = (int)rup(cr, 8);
   if (!(cr8 == 32 || cr8 == 64) || co % 8 != 0 || co > 64) return false;
   DirectGeo q{};
-  if (s->w % 32 == 0) q.TW = 32;
-  else if (s->w % 16 == 0) q.TW = 16;
+  const int gw = s->wo, gh = s->ho;                 // tile grid: output map, or the class positions
+  if (gw % 32 == 0) q.TW = 32;
+  else if (gw % 16 == 0) q.TW = 16;
   else return false;
   q.TH = 256 / q.TW;
   q.CP = cr8 / 8;
   q.NCF = co <= 32 ? 1 : 2;
-  q.tiles_x = s->w / q.TW;
-  q.tiles_y = cdiv(s->h, q.TH);
+  q.S2 = s2;
+  if (s2 && q.CP == 4 && q.NCF == 2) return false;   // not instantiated (launch_dgrad2_t)
+  q.tiles_x = gw / q.TW;
+  q.tiles_y = cdiv(gh, q.TH);
   q.ntiles = (long)s->n * q.tiles_x * q.tiles_y;
   if (q.ntiles >= (1l << 30)) return false;
-  const int occ = (q.TW == 32 ? (q.CP == 8 ? (q.NCF == 2 ? DirGeo<32, 8, 2>::OCC : DirGeo<32, 8, 1>::OCC)
-                                            : (q.NCF == 2 ? DirGeo<32, 4, 2>::OCC : DirGeo<32, 4, 1>::OCC))
-                              : (q.CP == 8 ? (q.NCF == 2 ? DirGeo<16, 8, 2>::OCC : DirGeo<16, 8, 1>::OCC)
-                                            : (q.NCF == 2 ? DirGeo<16, 4, 2>::OCC : DirGeo<16, 4, 1>::OCC)));
+  const int occ = s2 ? direct_occ<DirGeo2>(q.TW, q.CP, q.NCF) : direct_occ<DirGeo>(q.TW, q.CP, q.NCF);
   q.grid = (int)std::max<long>(1, std::min<long>(q.ntiles, (long)occ * conv_cu_count()));
   *g = q;
   return true;
@@ -501,8 +744,49 @@ static void launch_direct_epi(const DirectParams& p, int mode, int epi, int grid
   }
 }
 
+template <typename T, int TW, int CP, int NCF>
+static void launch_dgrad2(const DirectParams& p, int epi, int grid, hipStream_t st) {
+  using G = DirGeo2<TW, CP, NCF>;
+  auto k = epi == EPI_ACCUM ? conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_ACCUM>
+                            : conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_STORE>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_ACCUM>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    (void)hipFuncSetAttribute((const void*)conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_STORE>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    attr = true;
+  }
+  hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(G::NTHR), G::LDS, st, p);
+}
+
+// (32 reduction channels with 33..64 outputs is not instantiated: at two blocks per CU its four
+// classes' accumulate operands do not fit the registers; conv_direct_geometry routes it to the NT kernel)
+template <typename T>
+static void launch_dgrad2_t(const DirectGeo& g, const DirectParams& p, int epi, hipStream_t st) {
+  if (g.TW == 32) {
+    if (g.CP == 8) {
+      if (g.NCF == 2) launch_dgrad2<T, 32, 8, 2>(p, epi, g.grid, st);
+      else launch_dgrad2<T, 32, 8, 1>(p, epi, g.grid, st);
+    } else {
+      launch_dgrad2<T, 32, 4, 1>(p, epi, g.grid, st);
+    }
+  } else {
+    if (g.CP == 8) {
+      if (g.NCF == 2) launch_dgrad2<T, 16, 8, 2>(p, epi, g.grid, st);
+      else launch_dgrad2<T, 16, 8, 1>(p, epi, g.grid, st);
+    } else {
+      launch_dgrad2<T, 16, 4, 1>(p, epi, g.grid, st);
+    }
+  }
+}
+
 template <typename T>
 static void launch_direct_t(const DirectGeo& g, const DirectParams& p, int mode, int epi, hipStream_t st) {
+  if (g.S2) {
+    launch_dgrad2_t<T>(g, p, epi, st);
+    return;
+  }
   if (g.TW == 32) {
     if (g.CP == 8) {
       if (g.NCF == 2) launch_direct_epi<T, 32, 8, 2>(p, mode, epi, g.grid, st);
@@ -534,12 +818,15 @@ yms_status conv_direct_launch(const yms_conv_shape* s, int mode, const DirectGeo
   p.src_ld = src_ld; p.src_off = src_off; p.dst_ld = dst_ld; p.dst_off = dst_off;
   p.res_ld = res_ld; p.res_off = res_off;
   p.scale = scale; p.shift = shift; p.act = act;
-  p.H = s->h; p.W = s->w;
+  // source map: x (forward) or dz (input gradient); output map: y or dx
+  p.H = mode == 0 ? s->h : s->ho; p.W = mode == 0 ? s->w : s->wo;
+  p.OH = mode == 0 ? s->ho : s->h; p.OW = mode == 0 ? s->wo : s->w;
   p.tiles_x = g.tiles_x; p.tiles_y = g.tiles_y; p.ntiles = (int)g.ntiles;
   p.Ncols = mode == 0 ? s->cout : s->cin;
   p.nkt = (9 * g.CP + 7) / 8;      // the packed row pitch of yms_conv_pack_weight (fwd and stride-1 dgrad)
-  const long pix = (long)s->n * s->h * s->w;
-  const long sb = pix * src_ld * 2, db = pix * dst_ld * 2, rb = res ? pix * res_ld * 2 : 0;
+  p.wrows = (int)rup(p.Ncols, 128);  // rows of the stride-2 class blocks (yms_conv_pack_weight, dg2_geo)
+  const long spix = (long)s->n * p.H * p.W, opix = (long)s->n * p.OH * p.OW;
+  const long sb = spix * src_ld * 2, db = opix * dst_ld * 2, rb = res ? opix * res_ld * 2 : 0;
   const long lim = (1l << 31) - (1l << 20);
   if (sb >= lim || db >= lim || rb >= lim) return YMS_ERR_UNSUPPORTED;
   p.src_bytes = (uint32_t)sb;

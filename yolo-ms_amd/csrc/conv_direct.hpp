@@ -9,14 +9,16 @@ struct DirectGeo {
   int TW, TH;            // output tile (TW divides the map width)
   int CP;                // 16-B chunks of reduction channels per pixel (4 or 8)
   int NCF;               // 32-column MFMA fragments of output channels (1 or 2)
+  bool S2;               // stride-2 input gradient (tiles of class positions)
   int tiles_x, tiles_y;
   long ntiles;
   int grid;              // persistent blocks (= statistics rows of a training forward)
 };
 
-// True when the direct kernel runs this conv: 16-bit, 3x3, stride 1, pad 1, reduction channels
-// rounded to 8 of 32 or 64, at most 64 output channels (a multiple of 8), map width a multiple of
-// 16.  mode 0 = forward (reduction = cin), 1 = stride-1 input gradient (reduction = cout).
+// True when the direct kernel runs this conv: 16-bit, 3x3, pad 1, reduction channels rounded to
+// 8 of 32 or 64, at most 64 output channels (a multiple of 8), map width a multiple of 16.
+// mode 0 = stride-1 forward (reduction = cin), 1 = input gradient (reduction = cout) of a stride-1
+// conv, or of a stride-2 conv by output parity class (grid width ceil(w / 2) a multiple of 16).
 // YMS_DIRECT=0 turns it off (A/B and tests; read per call).
 bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g);
 
