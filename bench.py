@@ -149,8 +149,7 @@ def conv_roofline(prof, label):
 
 
 VALU_F32_PEAK_TFLOPS = 157.3    # fp32 vector FMA rate, MI355X_MICROARCH.md chip table
-DW_NAMES = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_dgrad_bnred", "yms_dwconv_wgrad", "yms_dwconv_fwd_bnin",
-            "yms_dwconv_wgrad_bnin")
+DW_NAMES = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
 BN_NAMES = ("yms_bn_act_bwd_reduce", "yms_bn_act_bwd_apply", "yms_affine_act", "yms_add_views", "yms_add_grad2")
 
 
@@ -329,14 +328,13 @@ def cpu_baseline_infer(version, nc, size, batch=8, steps=12):
 
 def make_sgd(params):
     """The reference's SGD-nesterov step (train.py optimizer settings); one fused multi-tensor
-    kernel where torch has it for this device (YMS_SGD=foreach forces the foreach kernels)."""
+    kernel where torch has it for this device, else the foreach kernels."""
     kw = dict(lr=0.01, momentum=0.937, nesterov=True, weight_decay=5e-4)
     params = list(params)
-    if os.environ.get("YMS_SGD", "fused") == "fused":
-        try:
-            return torch.optim.SGD(params, fused=True, **kw)
-        except (RuntimeError, TypeError, ValueError):
-            pass
+    try:
+        return torch.optim.SGD(params, fused=True, **kw)
+    except (RuntimeError, TypeError, ValueError):
+        pass
     return torch.optim.SGD(params, foreach=True, **kw)
 
 

@@ -229,34 +229,13 @@ int yms_dwconv_stats_rows(const yms_dw_shape* s);
 yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
                           int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
                           int stats_ld, void* stream);
-/* Training forward (statistics as yms_dwconv_fwd) whose input x = in_act(z * in_scale + in_shift)
- * per channel is never materialised: the producer's pre-BN z is read and transformed in LDS once
- * per element (zero padding stays zero) -- the producer's affine_act pass goes (16-bit only). */
-yms_status yms_dwconv_fwd_bnin(const yms_dw_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
-                               const float* in_shift, int in_act, const float* w, void* y, int y_ld, int y_off,
-                               float* stats, int stats_ld, void* stream);
 /* dx (+)= depthwise conv of dz with the 180-degree rotated kernel */
 yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w, void* dx,
                             int dx_ld, int dx_off, int accumulate, void* stream);
-/* Fused: dx = depthwise conv of dz with the rotated kernel (store, never accumulate), where dx is
- * the WHOLE gradient of the producer's activation a = act(BN(rz)) (the producer's only consumer is
- * this conv), plus the producer's BN + act backward partial sums over dx as stored: rows
- * [yms_dwconv_dgrad_rows][2][c] of (sum da, sum da * (rz - mean) * invstd), da = dx * act'(rz * rscale
- * + rshift) -- the layout yms_bn_act_bwd_finalize takes (replaces yms_bn_act_bwd_reduce of the
- * producer, which re-read dx and rz).  rmean_invstd = [mean | invstd] of the producer's BN. */
-int yms_dwconv_dgrad_rows(const yms_dw_shape* s);
-yms_status yms_dwconv_dgrad_bnred(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w,
-                                  void* dx, int dx_ld, int dx_off, const void* rz, int rz_ld, int rz_off,
-                                  const float* rscale, const float* rshift, const float* rmean_invstd, int ract,
-                                  float* rws, void* stream);
 /* dw[c][t] (+)= sum_pixels x(p + d_t) dz(p), fp32, via per-block partials in ws (deterministic) */
 size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s);
 yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
                             int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream);
-/* yms_dwconv_wgrad with x = in_act(z * in_scale + in_shift) formed from z while staging (16-bit) */
-yms_status yms_dwconv_wgrad_bnin(const yms_dw_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
-                                 const float* in_shift, int in_act, const void* dz, int dz_ld, int dz_off, float* ws,
-                                 size_t ws_bytes, float* dw, int accumulate, void* stream);
 /* y (+)= a + b over npix x c channels (b may be NULL); c % 8 == 0 */
 yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,
                          int b_off, void* y, int y_ld, int y_off, int accumulate, void* stream);

@@ -165,13 +165,15 @@ def _flat(st, cnt):
     return torch.as_strided(base, (base.numel() + cnt.numel(),), (1,))
 
 
-# SPPF pool backward: the whole-map fused kernel (argmax + gather in LDS, one launch per pool) must
-# reproduce the two-kernel path bit for bit -- ties (quantised values), NaNs, map sizes of every
-# channel-group width (<= 400, <= 800, <= 1600 pixels), channel counts not a multiple of the group
+# SPPF pool backward (argmax + gather per pool, slot 3 -> 2 -> 1 -> 0) against torch's CPU
+# max_pool2d backward on the kernel's own forward slots: PyTorch scan order with the first max and
+# NaN-propagating comparisons -- ties (quantised values), NaNs, maps of every size class, channel
+# counts not a multiple of 16; each slot's gradient rounded to the dtype before it feeds the next pool
 @pytest.mark.parametrize("n,h,w,c", [(2, 20, 20, 64), (1, 13, 17, 40), (2, 24, 30, 48), (1, 40, 40, 24),
                                      (3, 5, 7, 16)])
 @pytest.mark.parametrize("dt", [torch.bfloat16, torch.float16])
-def test_sppf_pool_bwd_fused_matches_two_kernel(n, h, w, c, dt, monkeypatch):
+def test_sppf_pool_bwd_matches_torch(n, h, w, c, dt):
+    import torch.nn.functional as F
     g = torch.Generator().manual_seed(n * 100 + h + w + c)
     ld = 4 * c + 8
     # slots 0..3 of an NHWC concat buffer at channel offset 8; quantised values give many ties
@@ -183,17 +185,29 @@ def test_sppf_pool_bwd_fused_matches_two_kernel(n, h, w, c, dt, monkeypatch):
     L.call("yms_sppf_pool_fwd", L.dtype_code(dt), n, h, w, c, buf.data_ptr(), ld, 8, L.stream_ptr())
     g0 = torch.randn(n, h, w, ld, generator=g).to(dt).cuda()
     ws = torch.empty(n * h * w * ((c + 7) // 8) * 8, dtype=torch.uint8, device="cuda")
-    outs = []
-    for fused in ("0", "1"):
-        monkeypatch.setenv("YMS_SPPF_FUSED", fused)
-        gb = g0.clone()
-        L.call("yms_sppf_pool_bwd", L.dtype_code(dt), n, h, w, c, buf.data_ptr(), ld, 8, gb.data_ptr(), ld, 8,
-               ws.data_ptr(), L.stream_ptr())
-        torch.cuda.synchronize()
-        outs.append(gb.float().cpu())
-    a, b = outs
-    assert torch.equal(torch.isnan(a), torch.isnan(b))
-    assert torch.equal(torch.nan_to_num(a), torch.nan_to_num(b))
+    gb = g0.clone()
+    L.call("yms_sppf_pool_bwd", L.dtype_code(dt), n, h, w, c, buf.data_ptr(), ld, 8, gb.data_ptr(), ld, 8,
+           ws.data_ptr(), L.stream_ptr())
+    torch.cuda.synchronize()
+    xs = buf.float().cpu()
+    ref = g0.float().cpu()
+
+    def slot(t, k):
+        return t[..., 8 + k * c:8 + (k + 1) * c].permute(0, 3, 1, 2)
+
+    for k in (3, 2, 1):
+        xin = slot(xs, k - 1).contiguous().requires_grad_(True)
+        y = F.max_pool2d(xin, 5, 1, 2)
+        assert torch.equal(torch.isnan(y), torch.isnan(slot(xs, k)))
+        y.backward(slot(ref, k).contiguous())
+        ref[..., 8 + (k - 1) * c:8 + k * c] = (slot(ref, k - 1) + xin.grad).to(dt).float().permute(0, 2, 3, 1)
+    got = gb.float().cpu()
+    assert torch.equal(got[..., 8 + 3 * c:], ref[..., 8 + 3 * c:])      # slot 3 (the last pool's output)
+    assert torch.equal(got[..., :8], ref[..., :8])
+    # fp32 sums of the same addends in another order: one rounding step of the dtype at most
+    tol = 2 ** -7 if dt == torch.bfloat16 else 2 ** -10
+    d = (got - ref).abs()
+    assert (d <= tol * ref.abs() + 1e-6).all(), d.max().item()
 
 
 @pytest.mark.parametrize("npix,c,ld,off", [(44800, 64, 64, 0), (40001, 24, 40, 8), (100, 16, 16, 0),
@@ -201,10 +215,10 @@ def test_sppf_pool_bwd_fused_matches_two_kernel(n, h, w, c, dt, monkeypatch):
                                            (7 * 80 * 80, 128, 256, 128)])
 @pytest.mark.parametrize("dt", ["bf16", "f16", "f32"])
 @pytest.mark.parametrize("has_z", [True, False])
-def test_bn_bwd_reduce_pipelined_matches_serial(npix, c, ld, off, dt, has_z, monkeypatch):
-    """The software-pipelined reduce loop (c % 8 == 0, unconditional loads with the tail pixels
-    re-read and masked) sums in the serial loop's order; the two loops may contract a different
-    set of mul+add pairs into FMAs, so partial rows agree to fp32 rounding, not bit for bit."""
+def test_bn_bwd_reduce_partial_rows(npix, c, ld, off, dt, has_z):
+    """The software-pipelined reduce (unconditional loads with the tail pixels re-read and masked):
+    exactly yms_bn_bwd_rows partial rows written, summing to the fp64 (sum da, sum da * xhat) of the
+    same dtype-rounded pixels; without z the rows carry sum gy (bias gradient)."""
     tdt, code = {"bf16": (torch.bfloat16, L.BF16), "f16": (torch.float16, L.F16), "f32": (torch.float32, L.F32)}[dt]
     g = torch.Generator().manual_seed(npix * 7 + c)
     z = torch.randn(npix, ld, generator=g).to(tdt).cuda()
@@ -213,36 +227,34 @@ def test_bn_bwd_reduce_pipelined_matches_serial(npix, c, ld, off, dt, has_z, mon
     sh = (torch.randn(c, generator=g) * 0.2).cuda()
     mi = torch.cat([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5]).cuda()
     rows = L.lib().yms_bn_bwd_rows(npix, c)
-    outs = []
-    for pipe in ("0", "1"):
-        monkeypatch.setenv("YMS_BN_RED_PIPE", pipe)
-        ws = torch.full((rows + 4, 2, c), float("nan"), device="cuda")
-        L.call("yms_bn_act_bwd_reduce", code, npix, c, z.data_ptr() if has_z else None, ld, off, gy.data_ptr(), ld,
-               off, sc.data_ptr(), sh.data_ptr(), mi.data_ptr(), 1, ws.data_ptr(), L.stream_ptr())
-        torch.cuda.synchronize()
-        assert torch.isnan(ws[rows:]).all() and torch.isfinite(ws[:rows]).all()
-        outs.append(ws[:rows].cpu())
-    assert ((outs[0] - outs[1]).norm() / outs[0].norm()).item() < 1e-6
-    if has_z and dt == "f32":          # and the sums are the op's (fp64 reference of the same pixels)
-        zz, gg = z[:, off:off + c].double().cpu(), gy[:, off:off + c].double().cpu()
-        a = zz * sc.double().cpu() + sh.double().cpu()
-        s = torch.sigmoid(a)
-        da = gg * (s * (1 + a * (1 - s)))
-        xh = (zz - mi[:c].double().cpu()) * mi[c:].double().cpu()
-        tot = outs[1].double().sum(0)
-        assert ((tot[0] - da.sum(0)).norm() / da.sum(0).norm()).item() < 1e-5
-        assert ((tot[1] - (da * xh).sum(0)).norm() / (da * xh).sum(0).norm()).item() < 1e-5
+    ws = torch.full((rows + 4, 2, c), float("nan"), device="cuda")
+    L.call("yms_bn_act_bwd_reduce", code, npix, c, z.data_ptr() if has_z else None, ld, off, gy.data_ptr(), ld,
+           off, sc.data_ptr(), sh.data_ptr(), mi.data_ptr(), 1, ws.data_ptr(), L.stream_ptr())
+    torch.cuda.synchronize()
+    assert torch.isnan(ws[rows:]).all() and torch.isfinite(ws[:rows]).all()
+    tot = ws[:rows].double().sum(0).cpu()
+    gg = gy[:, off:off + c].double().cpu()
+    if not has_z:
+        assert ((tot[0] - gg.sum(0)).norm() / gg.sum(0).norm()).item() < 1e-5
+        return
+    zz = z[:, off:off + c].double().cpu()
+    a = zz * sc.double().cpu() + sh.double().cpu()
+    s = torch.sigmoid(a)
+    da = gg * (s * (1 + a * (1 - s)))
+    xh = (zz - mi[:c].double().cpu()) * mi[c:].double().cpu()
+    assert ((tot[0] - da.sum(0)).norm() / da.sum(0).norm()).item() < 1e-5
+    assert ((tot[1] - (da * xh).sum(0)).norm() / (da * xh).sum(0).norm()).item() < 1e-5
 
 
 @pytest.mark.parametrize("npix,c,ld", [(44801, 64, 64), (3001, 40, 48), (25600, 768, 776), (999, 24, 32)])
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
 @pytest.mark.parametrize("gres_mode", [0, 1, 2])          # no residual gradient / store / accumulate
 @pytest.mark.parametrize("inplace", [False, True])         # dz written over z (the plan's default)
-@pytest.mark.parametrize("iters", ["4", "16"])
-def test_bn_bwd_apply_pipelined_matches_serial(npix, c, ld, dt, gres_mode, inplace, iters, monkeypatch):
-    """The software-pipelined apply loop (YMS_BN_APPLY_PIPE=1) against the serial loop: same dz and
-    residual gradient, including dz over z in place and an accumulated residual gradient (masked
-    stores: a clamped duplicate pixel is never written twice)."""
+def test_bn_bwd_apply_matches_fp64(npix, c, ld, dt, gres_mode, inplace):
+    """The software-pipelined apply pass against fp64 of the same formula: dz = scale (da - coef0 -
+    xhat coef1) and the residual gradient (gy, or r + gy), including dz over z in place and an
+    accumulated residual gradient (masked stores: a clamped duplicate pixel is never written twice);
+    the pad columns past c stay untouched."""
     tdt, code = {"bf16": (torch.bfloat16, L.BF16), "f32": (torch.float32, L.F32)}[dt]
     g = torch.Generator().manual_seed(npix + c + gres_mode)
     z0 = torch.randn(npix, ld, generator=g).to(tdt).cuda()
@@ -252,48 +264,60 @@ def test_bn_bwd_apply_pipelined_matches_serial(npix, c, ld, dt, gres_mode, inpla
     sh = (torch.randn(c, generator=g) * 0.2).cuda()
     mi = torch.cat([torch.randn(c, generator=g) * 0.1, torch.rand(c, generator=g) + 0.5]).cuda()
     coef = (torch.randn(2 * c, generator=g) * 0.1).cuda()
-    monkeypatch.setenv("YMS_BN_APPLY_ITERS", iters)
-    outs = []
-    for pipe in ("0", "1"):
-        monkeypatch.setenv("YMS_BN_APPLY_PIPE", pipe)
-        z = z0.clone()
-        dz = z if inplace else torch.full_like(z0, 7.0)
-        r = r0.clone()
-        L.call("yms_bn_act_bwd_apply", code, npix, c, z.data_ptr(), ld, 0, gy.data_ptr(), ld, 0, sc.data_ptr(),
-               sh.data_ptr(), mi.data_ptr(), coef.data_ptr(), 1, dz.data_ptr(), ld, 0,
-               r.data_ptr() if gres_mode else None, ld, 0, int(gres_mode == 2), L.stream_ptr())
-        torch.cuda.synchronize()
-        outs.append((dz.float().cpu(), r.float().cpu()))
-    (d0, q0), (d1, q1) = outs
-    assert torch.equal(d0[:, c:], d1[:, c:]) and torch.equal(q0[:, c:], q1[:, c:])    # pad columns untouched
-    tol = 1e-6 if dt == "f32" else 1e-2
-    assert ((d0 - d1).abs().max() <= tol * (1 + d0.abs().max())).item()
-    assert torch.equal(q0, q1)           # the residual gradient is gy or r + gy: no FMA to contract
+    z = z0.clone()
+    dz = z if inplace else torch.full_like(z0, 7.0)
+    r = r0.clone()
+    L.call("yms_bn_act_bwd_apply", code, npix, c, z.data_ptr(), ld, 0, gy.data_ptr(), ld, 0, sc.data_ptr(),
+           sh.data_ptr(), mi.data_ptr(), coef.data_ptr(), 1, dz.data_ptr(), ld, 0,
+           r.data_ptr() if gres_mode else None, ld, 0, int(gres_mode == 2), L.stream_ptr())
+    torch.cuda.synchronize()
+    zz, gg = z0[:, :c].double().cpu(), gy[:, :c].double().cpu()
+    scd, cf = sc.double().cpu(), coef.double().cpu()
+    a = zz * scd + sh.double().cpu()
+    s = torch.sigmoid(a)
+    da = gg * (s * (1 + a * (1 - s)))
+    xh = (zz - mi[:c].double().cpu()) * mi[c:].double().cpu()
+    ref = scd * (da - cf[:c] - xh * cf[c:])
+    got = dz.double().cpu()
+    tol = 1e-5 if dt == "f32" else 1e-2
+    assert ((got[:, :c] - ref).abs().max() <= tol * (1 + ref.abs().max())).item()
+    pad = z0 if inplace else torch.full_like(z0, 7.0)
+    assert torch.equal(dz[:, c:], pad[:, c:])
+    rr = r.double().cpu()
+    if gres_mode == 0:
+        assert torch.equal(r, r0)
+    else:
+        want = gy[:, :c].double().cpu() + (r0[:, :c].double().cpu() if gres_mode == 2 else 0)
+        assert torch.equal(rr[:, :c], want.to(tdt).double())
+        assert torch.equal(r[:, c:], r0[:, c:])
 
 
 @pytest.mark.parametrize("npix,c,ld", [(44801, 64, 64), (3001, 40, 48), (25600, 768, 776), (999, 24, 32)])
 @pytest.mark.parametrize("dt", ["bf16", "f32"])
 @pytest.mark.parametrize("res_mode", [0, 1, 2])            # no residual / residual / y written over the residual
-@pytest.mark.parametrize("iters", ["2", "8"])
-def test_affine_act_pipelined_matches_serial(npix, c, ld, dt, res_mode, iters, monkeypatch):
-    """The software-pipelined forward BN+SiLU(+res) pass (YMS_BN_AFFINE_PIPE=1) against the
-    serial loop, ragged pixel counts and an in-place residual included."""
+def test_affine_act_matches_fp64(npix, c, ld, dt, res_mode):
+    """The software-pipelined forward BN+SiLU(+res) pass against fp64 of the same formula, ragged
+    pixel counts and an in-place residual included; pad columns untouched."""
     tdt, code = {"bf16": (torch.bfloat16, L.BF16), "f32": (torch.float32, L.F32)}[dt]
     g = torch.Generator().manual_seed(npix + c + res_mode)
     z = torch.randn(npix, ld, generator=g).to(tdt).cuda()
     r0 = torch.randn(npix, ld, generator=g).to(tdt).cuda()
     sc = (torch.rand(c, generator=g) + 0.5).cuda()
     sh = (torch.randn(c, generator=g) * 0.2).cuda()
-    monkeypatch.setenv("YMS_BN_AFFINE_ITERS", iters)
-    outs = []
-    for pipe in ("0", "1"):
-        monkeypatch.setenv("YMS_BN_AFFINE_PIPE", pipe)
-        r = r0.clone()
-        y = r if res_mode == 2 else torch.full_like(z, 7.0)
-        L.call("yms_affine_act", code, npix, c, z.data_ptr(), ld, 0, sc.data_ptr(), sh.data_ptr(), 1,
-               r.data_ptr() if res_mode else None, ld, 0, y.data_ptr(), ld, 0, L.stream_ptr())
-        torch.cuda.synchronize()
-        outs.append(y.float().cpu())
-    assert torch.equal(outs[0][:, c:], outs[1][:, c:])
+    r = r0.clone()
+    y = r if res_mode == 2 else torch.full_like(z, 7.0)
+    L.call("yms_affine_act", code, npix, c, z.data_ptr(), ld, 0, sc.data_ptr(), sh.data_ptr(), 1,
+           r.data_ptr() if res_mode else None, ld, 0, y.data_ptr(), ld, 0, L.stream_ptr())
+    torch.cuda.synchronize()
+    ref = F_silu(z[:, :c].double().cpu() * sc.double().cpu() + sh.double().cpu())
+    if res_mode:
+        ref = ref + r0[:, :c].double().cpu()
+    got = y.double().cpu()
     tol = 1e-6 if dt == "f32" else 1e-2
-    assert ((outs[0] - outs[1]).abs().max() <= tol * (1 + outs[0].abs().max())).item()
+    assert ((got[:, :c] - ref).abs().max() <= tol * (1 + ref.abs().max())).item()
+    pad = r0 if res_mode == 2 else torch.full_like(z, 7.0)
+    assert torch.equal(y[:, c:], pad[:, c:])
+
+
+def F_silu(a):
+    return a * torch.sigmoid(a)

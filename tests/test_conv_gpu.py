@@ -276,7 +276,7 @@ def test_wgrad_3x3_halo(shp, dt, mode, monkeypatch):
 # LDS-DMA ring weight gradient (wgrad_ring.hip): 1x1 and 3x3, stride 1 / 2, 64- and 128-row tiles
 # (cout 48, 64, 80, 128, 130, 256), 64-column GEMMs (1x1 with cin <= 64 on 128-row tiles), cin
 # not a multiple of 64 (40, 96, 200), pixel counts not a multiple of the k-tile, many splits,
-# channel slots of wider buffers; every ring variant (KP 64 / ST 2, KP 32 / ST 4, KP 64 / ST 3)
+# channel slots of wider buffers
 WGR = [
     (2, 64, 40, 40, 128, 3, 1), (3, 40, 13, 27, 48, 3, 1), (2, 96, 20, 20, 80, 1, 1), (1, 200, 17, 19, 130, 1, 1),
     (2, 32, 33, 41, 256, 3, 2), (2, 64, 24, 24, 64, 1, 1), (4, 128, 20, 20, 256, 3, 1), (2, 48, 9, 5, 96, 3, 2),
@@ -284,13 +284,11 @@ WGR = [
 ]
 
 
-@pytest.mark.parametrize("var", ["0", "1", "2", "3"])
 @pytest.mark.parametrize("dt", ["bf16", "f16"])
 @pytest.mark.parametrize("shp", WGR)
-def test_wgrad_ring(shp, dt, var, monkeypatch):
+def test_wgrad_ring(shp, dt, monkeypatch):
     monkeypatch.setenv("YMS_WG_HALO", "0")
     monkeypatch.setenv("YMS_WG_RING", "2")
-    monkeypatch.setenv("YMS_WG_RING_VAR", var)
     n, cin, h, w, cout, k, s = shp
     dtype = DT[dt]
     g = torch.Generator().manual_seed(n * 7919 + cin * 31 + h + w + cout + s + k)
@@ -343,3 +341,36 @@ def test_wgrad_split_k_slab_cap(route, ratio, monkeypatch):
         L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0,
                ws.data_ptr(), wsb, dw.data_ptr(), 0, L.stream_ptr())
         _close(dw.cpu(), wr.grad, 2e-3)
+
+
+@pytest.mark.parametrize("route", ["tt", "ring", "halo"])
+def test_wgrad_workspace_smaller_than_planned(route, monkeypatch):
+    """A workspace sized under other YMS_WG_* settings than the call's (here: fewer bytes than
+    yms_conv_wgrad_ws_bytes asks for) runs fewer split-K partial slabs instead of failing: the
+    gradient still matches; below one slab the call is refused."""
+    monkeypatch.setenv("YMS_WG_SLAB_RATIO", "1.0")       # many splits, so the shrink has room
+    monkeypatch.setenv("YMS_WG_RING", "1" if route == "ring" else "0")
+    monkeypatch.setenv("YMS_WG_HALO", "1" if route == "halo" else "0")
+    dtype = torch.bfloat16
+    n, cin, h, w, cout, k, s = (8, 64, 40, 40, 64, 3, 1) if route != "ring" else (8, 128, 20, 20, 256, 1, 1)
+    g = torch.Generator().manual_seed(11)
+    x = torch.randn(n, cin, h, w, generator=g)
+    shp_ = shape(n, h, w, cin, cout, k, s, dtype)
+    dz = torch.randn(n, cout, shp_.ho, shp_.wo, generator=g)
+    wr = torch.zeros(cout, cin, k, k, requires_grad=True)
+    F.conv2d(x.to(dtype).float(), wr, None, s, k // 2).backward(dz.to(dtype).float())
+    sp = ctypes.pointer(shp_)
+    xb, dzb = nhwc(x, dtype), nhwc(dz, dtype)
+    full = L.lib().yms_conv_wgrad_ws_bytes(sp)
+    slab = 4 * cout * k * k * cin                       # at least one slab (tiles round it up)
+    assert full > 2 * slab
+    for wsb in (full // 2 + 4, full // 3 + 4):
+        ws = torch.empty(wsb // 4 + 1, dtype=torch.float32, device="cuda")
+        dw = torch.zeros(cout, cin, k, k, device="cuda")
+        L.call("yms_conv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0,
+               ws.data_ptr(), wsb, dw.data_ptr(), 0, L.stream_ptr())
+        _close(dw.cpu(), wr.grad, 2e-3)
+    ws = torch.empty(16, dtype=torch.float32, device="cuda")
+    st = L.lib().yms_conv_wgrad(sp, xb.data_ptr(), xb.shape[-1], 0, dzb.data_ptr(), dzb.shape[-1], 0, ws.data_ptr(),
+                                64, dw.data_ptr(), 0, L.stream_ptr())
+    assert st != 0

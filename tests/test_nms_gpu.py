@@ -274,13 +274,11 @@ def _level_segments(B, seed, jitter=20.0, size=160.0):
     return pred
 
 
-@pytest.mark.parametrize("window", ["1", "0"])
-def test_window_and_kept_list_greedy_agree(monkeypatch, window):
-    """Big segments <= 8192 boxes on the opt-in window kernel (YMS_NMS_WINDOW=1) and on the default
-    kept-list grid greedy: both are bit-exact against the oracle on the bench's level segments, on dense
+def test_big_segment_greedy_bit_exact():
+    """Big segments <= 8192 boxes on the big-segment kernels (window-grid / kept-list grid greedy,
+    per the routing fixture): bit-exact against the oracle on the bench's level segments, on dense
     single-class segments, at thresholds 0.45 / 0.5 / 0.6 / 0 / negative, and with NaN / inf /
     zero-area boxes."""
-    monkeypatch.setenv("YMS_NMS_WINDOW", window)
     for thr in (0.45, 0.5, 0.6):
         assert _check(_level_segments(3, 21), 0.25, thr) > 0
     rng = np.random.default_rng(23)

@@ -1,13 +1,11 @@
-"""CPU tier for the plan's scratch ownership and the depthwise fusion selection (plans built on
-meta tensors, no GPU): every backward scratch region is its own range of the grad arena -- the
-side stream's weight gradients use only "wgrad", the main stream the others -- and the opt-in
-MS-Block IB fusions (YMS_DW_BNIN / YMS_DW_BNRED, yms/plan.py Plan._find_dw_bnred) pick exactly the
-expand-conv -> depthwise pairs of yolov8/model/yolo_ms.py MSBlockLayer."""
+"""CPU tier for the plan's scratch ownership (plans built on meta tensors, no GPU): every backward
+scratch region is its own range of the grad arena -- the side stream's weight gradients use only
+"wgrad", the main stream the others."""
 import pytest
 import torch
 
 from yms import runner
-from yms.plan import ConvOp, DWConvOp
+from yms.plan import ConvOp
 from yolov8.yolov8 import YOLOv8
 
 
@@ -30,33 +28,3 @@ def test_grad_scratch_regions_are_disjoint_and_sized(v):
     for op in p.ops:
         if isinstance(op, ConvOp) and type(op) is ConvOp and op.stem_input is None:
             assert op.wg_ws <= p.scratch_req["wgrad"]
-
-
-def test_dw_fusions_off_by_default():
-    p = _plan("ms-s")
-    for op in p.ops:
-        if type(op) is DWConvOp:
-            assert op.bnin is None and op.bnred is None
-        if type(op) is ConvOp:
-            assert op.bnin_by is None and op.red_rows == 0
-
-
-@pytest.mark.parametrize("which", ["YMS_DW_BNIN", "YMS_DW_BNRED"])
-def test_dw_fusion_pairs(which, monkeypatch):
-    monkeypatch.setenv(which, "1")
-    p = _plan("ms-s")
-    pairs = 0
-    for i, op in enumerate(p.ops):
-        if type(op) is not DWConvOp:
-            continue
-        prod = op.bnin if which == "YMS_DW_BNIN" else op.bnred
-        assert prod is p.ops[i - 1] and type(prod) is ConvOp and prod.y.buf is op.x.buf
-        readers = [o for o in p.ops if o is not prod and any(getattr(a, "buf", None) is op.x.buf
-                                                             for a in vars(o).values())]
-        assert readers == [op]
-        if which == "YMS_DW_BNIN":
-            assert prod.bnin_by is op
-        else:
-            assert prod.red_rows > 0 and 4 * 2 * prod.c * prod.red_rows <= p.scratch_req["bwd"]
-        pairs += 1
-    assert pairs == sum(1 for op in p.ops if type(op) is DWConvOp) > 0

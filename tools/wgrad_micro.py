@@ -39,15 +39,9 @@ torch.cuda.empty_cache()
 CONFIGS = {
     "old": {"YMS_WG_HALO": "0", "YMS_WG_RING": "0"},
     "halo": {"YMS_WG_HALO": "1", "YMS_WG_RING": "0"},
-    "ring0": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_RING_VAR": "0"},
-    "ring1": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_RING_VAR": "1"},
-    "ring2": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_RING_VAR": "2"},
-    "ring3": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_RING_VAR": "3"},
-    "ringall": {"YMS_WG_HALO": "0", "YMS_WG_RING": "2", "YMS_WG_RING_VAR": "0"},
-    "ringsmall": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_RING_VAR": "0", "YMS_WG_RING_SMALL": "1"},
+    "ring": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1"},
+    "ringall": {"YMS_WG_HALO": "0", "YMS_WG_RING": "2"},
 }
-for _c in CONFIGS.values():
-    _c.setdefault("YMS_WG_RING_SMALL", "0")
 sel = os.environ.get("YMS_WGM_CONFIGS")
 if sel:
     CONFIGS = {k: CONFIGS[k] for k in sel.split(",")}

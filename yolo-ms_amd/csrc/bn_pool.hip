@@ -174,7 +174,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* s
 // 1024-thread kernel above runs a 7-level tree with two barriers per level).  In the forward no
 // side-stream work competes for CU slots, so the finalize's latency is the step's.  Measured
 // step-neutral to slightly faster (YOLOv8-s 18.71 / 18.71 -> 18.67 / 18.74 ms, YOLO-MS-S 37.29 /
-// 37.37 -> 37.24 / 37.26 ms, profiles/r03u_bn_finalize_small_ab.txt); YMS_BN_FIN_SMALL=0 restores.
+// 37.37 -> 37.24 / 37.26 ms, profiles/r03u_bn_finalize_small_ab.txt).
 constexpr int FIN3_RL = 32;
 __global__ __launch_bounds__(256) void bn_finalize_small_kernel(int c, const float* stats, int rows, int ld,
                                                                 long count, const float* g, const float* b, float* rm,
@@ -338,7 +338,7 @@ struct BwdFin {          // fused finalize (FIN): the last reduce block to finis
   long count;
 };
 
-// PIPE = false: the serial loop for every c (YMS_BN_RED_PIPE=0, dev A/B)
+// PIPE = false: the serial loop for every c (c % 8 != 0 tails; the host launches PIPE = true)
 template <typename T, bool HAS_Z, bool FIN = false, bool PIPE = true>
 __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, const T* z, int z_ld,
                                                             int z_off, const T* gy, int gy_ld, int gy_off,
@@ -550,49 +550,6 @@ __global__ __launch_bounds__(32 * TY) void bn_bwd_finalize_kernel(int c, const f
   }
 }
 
-// latency-shaped variant (dev A/B, YMS_BN_FIN_V2=1): 8 channels x 32 row lanes, each lane issues
-// ALL its rows' loads before the first add -- one L2 round trip instead of a dependent chain of 16.
-// Measured slower in the step, interleaved on one box (round 3, profiles/r03q_bn_finalize_ab.txt):
-// YOLOv8-s 19.15-19.20 -> 19.32-19.36 ms, YOLO-MS-S 38.26 -> 38.56 ms.  Its 4x more blocks wait
-// for CU slots the side stream's weight-gradient blocks hold: inside the step the finalize's time
-// is slot waiting, not load latency (the same outcome as round 2's float4 variant).
-constexpr int FIN2_RL = 32, FIN2_MAXR = 16;
-__global__ __launch_bounds__(256) void bn_bwd_finalize2_kernel(int c, const float* ws, int rows, long count,
-                                                               float* dgamma, float* dbeta, float* coef) {
-  __shared__ double red[2][FIN2_RL][9];
-  const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
-  const int ch = blockIdx.x * 8 + tx;
-  double a1[4] = {0, 0, 0, 0}, a2[4] = {0, 0, 0, 0};
-  if (ch < c) {
-    for (int r0 = ty; r0 < rows; r0 += FIN2_RL * FIN2_MAXR) {
-      float v1[FIN2_MAXR], v2[FIN2_MAXR];
-#pragma unroll
-      for (int u = 0; u < FIN2_MAXR; ++u) {
-        const int r = r0 + FIN2_RL * u;
-        v1[u] = r < rows ? ws[(long)r * 2 * c + ch] : 0.f;
-        v2[u] = r < rows ? ws[(long)r * 2 * c + c + ch] : 0.f;
-      }
-#pragma unroll
-      for (int u = 0; u < FIN2_MAXR; ++u) {
-        a1[u & 3] += (double)v1[u];
-        a2[u & 3] += (double)v2[u];
-      }
-    }
-  }
-  red[0][ty][tx] = (a1[0] + a1[1]) + (a1[2] + a1[3]);
-  red[1][ty][tx] = (a2[0] + a2[1]) + (a2[2] + a2[3]);
-  __syncthreads();
-  if (ty == 0 && ch < c) {
-    double t1 = 0.0, t2 = 0.0;
-    for (int k = 0; k < FIN2_RL; ++k) { t1 += red[0][k][tx]; t2 += red[1][k][tx]; }
-    if (dbeta) dbeta[ch] = (float)t1;
-    if (dgamma) dgamma[ch] = (float)t2;
-    if (coef) {
-      coef[ch] = (float)(t1 / (double)count);
-      coef[c + ch] = (float)(t2 / (double)count);
-    }
-  }
-}
 
 // PIPE (the default): software-pipelined like the reduce (c % 8 == 0): the next U pixels' loads (clamped to
 // the block's last pixel, masked) are in flight while this U is computed and stored.  Stores stay
@@ -711,8 +668,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
 // ------------------------------------------------------------------------------------------
 // One MaxPool2d(5, 1, 2) of the SPPF chain: slot `out` = pool5(slot `in`) (-inf padding).
 // The chain p1 = pool(x), p2 = pool(p1), p3 = pool(p2) runs as three launches (75 loads per
-// output group instead of the 169 of a direct 13x13 window); max is exact, so the result is
-// bit-identical to the reference's chained pools.
+// output group instead of the 169 of a direct 13x13 window); max is exact and a NaN in the window
+// wins (torch's `val > max || isnan(val)`), so the result is bit-identical to the reference's chained
+// pools.
 template <typename T>
 __global__ __launch_bounds__(256) void pool5_fwd_kernel(int n, int h, int w, int c, T* buf, int ld, int in_off,
                                                         int out_off) {
@@ -733,7 +691,7 @@ __global__ __launch_bounds__(256) void pool5_fwd_kernel(int n, int h, int w, int
         float v[8];
         Vec8<T>::load(row + (long)xx * ld, v);
 #pragma unroll
-        for (int i = 0; i < 8; ++i) m[i] = fmaxf(m[i], v[i]);
+        for (int i = 0; i < 8; ++i) m[i] = (v[i] > m[i] || v[i] != v[i]) ? v[i] : m[i];   // NaN propagates (torch)
       }
     }
     Vec8<T>::store(buf + (long)pix * ld + out_off + g * 8, m);
@@ -820,89 +778,6 @@ __global__ void pool5_gather_kernel(int n, int h, int w, int c, const uint8_t* a
   }
 }
 
-// ------------------------------------------------------------------------------------------
-// SPPF pool backward, one launch per chained pool (maps of <= 1600 pixels: the 20^2 / 40^2 SPPF of
-// a 640 / 1280 input): a block owns one image x CG channels of the whole map, stages the pool's
-// input slot and the output-gradient slot in LDS, forms every output's window argmax there (the
-// loop of pool5_argmax_kernel: first maximum in row-major window order, NaN wins) and gathers
-// each input pixel's gradient from the 5 x 5 outputs that chose it, in the order of
-// pool5_gather_kernel -- the same argmax bytes and the same fp32 sums (bit-identical), one global
-// pass over the three slots instead of 25 scattered L2 loads per element in each of two launches.
-// Opt-in (see yms_sppf_pool_bwd): measured slower inside the training step.
-// ------------------------------------------------------------------------------------------
-template <typename T, int CG>
-__global__ __launch_bounds__(256) void pool5_bwd_fused_kernel(int h, int w, int c, const T* buf, int ld, int in_off,
-                                                              T* g, int gy_off, int gx_off) {
-  constexpr int NCH = CG / 8;                     // 16-B chunks per pixel in the block
-  extern __shared__ __attribute__((aligned(16))) char dsm[];
-  const int hw = h * w;
-  Raw8<T>* X = reinterpret_cast<Raw8<T>*>(dsm);
-  Raw8<T>* GY = X + hw * NCH;
-  uint8_t* ARG = reinterpret_cast<uint8_t*>(GY + hw * NCH);
-  const int b = blockIdx.x, c0 = blockIdx.y * CG;
-  const long img = (long)b * hw;
-  for (int it = threadIdx.x; it < hw * NCH; it += 256) {
-    const int pix = it / NCH, j = it - pix * NCH, cc = c0 + 8 * j;
-    const int nv = min(8, c - cc);
-    if (nv > 0) {
-      load_raw8(buf + (img + pix) * ld + in_off + cc, nv, X[it]);
-      load_raw8(g + (img + pix) * ld + gy_off + cc, nv, GY[it]);
-    }
-  }
-  __syncthreads();
-  for (int it = threadIdx.x; it < hw * NCH; it += 256) {
-    const int pix = it / NCH, j = it - pix * NCH;
-    const int y = pix / w, x = pix - y * w;
-    float best[8];
-    uint8_t idx[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) { best[i] = -INFINITY; idx[i] = 255; }
-    for (int ky = 0; ky < 5; ++ky) {
-      const int yy = y - 2 + ky;
-      if (yy < 0 || yy >= h) continue;
-      for (int kx = 0; kx < 5; ++kx) {
-        const int xx = x - 2 + kx;
-        if (xx < 0 || xx >= w) continue;
-        float v[8];
-        unpack8(X[(yy * w + xx) * NCH + j], v);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (idx[i] == 255 || v[i] > best[i] || v[i] != v[i]) {  // (val > maxval) || isnan(val)
-            best[i] = v[i];
-            idx[i] = (uint8_t)(ky * 5 + kx);
-          }
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) ARG[it * 8 + i] = idx[i];
-  }
-  __syncthreads();
-  for (int it = threadIdx.x; it < hw * NCH; it += 256) {
-    const int pix = it / NCH, j = it - pix * NCH, cc = c0 + 8 * j;
-    const int nv = min(8, c - cc);
-    if (nv <= 0) continue;
-    const int y = pix / w, x = pix - y * w;
-    T* dst = g + (img + pix) * ld + gx_off + cc;
-    float acc[8];
-    load8(dst, nv, acc);
-    for (int ky = 0; ky < 5; ++ky) {
-      const int oy = y - ky + 2;
-      if (oy < 0 || oy >= h) continue;
-      for (int kx = 0; kx < 5; ++kx) {
-        const int ox = x - kx + 2;
-        if (ox < 0 || ox >= w) continue;
-        const int o = (oy * w + ox) * NCH + j;
-        const uint8_t want = (uint8_t)(ky * 5 + kx);
-        float gv[8];
-        unpack8(GY[o], gv);
-#pragma unroll
-        for (int i = 0; i < 8; ++i)
-          if (ARG[o * 8 + i] == want) acc[i] += gv[i];
-      }
-    }
-    store8(dst, nv, acc);
-  }
-}
 
 // ------------------------------------------------------------------------------------------
 // nearest x2 upsample
@@ -1071,8 +946,7 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
     hipLaunchKernelGGL(bn_stats_partial_kernel, dim3(cdiv(c, 64), nrows), dim3(256), 0, (hipStream_t)stream, c,
                        stats, rows, stats_ld, rs);
   }
-  static const int small = getenv("YMS_BN_FIN_SMALL") ? atoi(getenv("YMS_BN_FIN_SMALL")) : 1;   // dev A/B
-  if (small && rs == 1) {
+  if (rs == 1) {
     hipLaunchKernelGGL(bn_finalize_small_kernel, dim3(cdiv(c, 8)), dim3(256), 0, (hipStream_t)stream, c,
                        (const float*)stats, rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps,
                        mean_invstd, scale, shift);
@@ -1090,11 +964,8 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
 static long elem_ppb(long npix, int c, int iters = 4) {
   const long py = 256 / ((c + 7) / 8);
   long blocks = std::min<long>(std::max<long>(cdiv(npix, py * BN_U * iters), 1), 8192);
-  // small layers (20^2 / 40^2 maps): at four iterations per thread they launch 100-400 blocks,
-  // 1-2 per CU, too few waves in flight for an HBM-bound pass; keep at least `minb` blocks while
-  // each thread still gets one full U-pixel iteration (YMS_BN_MINB, dev A/B)
-  static const long minb = getenv("YMS_BN_MINB") ? atol(getenv("YMS_BN_MINB")) : 0;
-  if (minb > 0) blocks = std::max<long>(blocks, std::min<long>(minb, cdiv(npix, py * BN_U)));
+  // (round 3: a floor of 1024-2048 blocks for the small 20^2 / 40^2 layers made the step slower,
+  // profiles/r03s_bn_minblocks_ab.txt: the extra blocks wait for CU slots the side stream holds)
   return (npix + blocks - 1) / blocks;
 }
 
@@ -1107,40 +978,29 @@ yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, 
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
   // two U-pixel iterations per thread: the forward affine pass (no side-stream work beside it) took
   // 1.73 / 1.74 ms per YOLOv8-s step against 1.80 / 1.80 at four, 3.66-3.68 vs 3.70-3.73 ms on
-  // YOLO-MS-S (interleaved, profiles/r03y_affine_iters_ab.txt); YMS_BN_AFFINE_ITERS overrides
-  // software-pipelined loop (the default; YMS_BN_AFFINE_PIPE=0 selects the serial loop): affine
-  // 1.72 -> 1.70 ms per YOLOv8-s step, 3.68 -> 3.57 ms on YOLO-MS-S, steps 18.20 -> 18.13 ms and
-  // 37.24 -> 37.12 ms (interleaved pairs; pipelined at 4 / 8 iterations slower,
-  // profiles/r03zg_affine_pipe_ab.txt).  Both knobs read per call.
-  const char* pe = getenv("YMS_BN_AFFINE_PIPE");
-  const bool pipe = !pe || atoi(pe) != 0;
-  const char* ie = getenv("YMS_BN_AFFINE_ITERS");
-  const int iters = ie ? std::max(1, atoi(ie)) : 2;
-  const long ppb = elem_ppb(npix, c, iters);
+  // YOLO-MS-S (interleaved, profiles/r03y_affine_iters_ab.txt)
+  // software-pipelined loop: affine 1.72 -> 1.70 ms per YOLOv8-s step, 3.68 -> 3.57 ms on YOLO-MS-S,
+  // steps 18.20 -> 18.13 ms and 37.24 -> 37.12 ms over the serial loop (interleaved pairs; pipelined
+  // at 4 / 8 iterations slower, profiles/r03zg_affine_pipe_ab.txt)
+  const long ppb = elem_ppb(npix, c, 2);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
-#define YMS_AFF(PP)                                                                                  \
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((affine_act_kernel<T, PP>), dim3(blocks), dim3(256), 0, \
-                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off, \
-                                               scale, shift, act, (const T*)res, res_ld, res_off, (T*)y, \
-                                               y_ld, y_off, ppb))
-  if (pipe) YMS_AFF(true);
-  else YMS_AFF(false);
-#undef YMS_AFF
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((affine_act_kernel<T, true>), dim3(blocks), dim3(256), 0,
+                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
+                                               scale, shift, act, (const T*)res, res_ld, res_off, (T*)y,
+                                               y_ld, y_off, ppb));
   return launch_status();
 }
 
 // pixels per BN-backward reduce block.  Partial-sum rows = reduce blocks, at most 256 with the
 // pipelined reduce loop (one block per CU; cap 128 / 256 / 384 / 512: 18.64 / 18.28 / 18.52 /
 // 18.74 ms per YOLOv8-s step, interleaved, profiles/r03ze_bn_reduce_pipe_cap_ab.txt).  With the
-// serial loop 512 was best (round 2: 1024 19.82 ms, 512 19.50, 256 19.53, 2048 20.33);
-// YMS_BN_BWD_ROWS_CAP overrides.  The fused
+// serial loop 512 was best (round 2: 1024 19.82 ms, 512 19.50, 256 19.53, 2048 20.33).  The fused
 // reduce + finalize (one last block sums the whole table) also keeps rows <= 32768 / c (table
 // <= 256 KB); the two-kernel path does not: that cap left 64-128 reduce blocks on 256 CUs for
 // the 256/512-channel layers (interleaved A/B: YOLOv8-s 19.51 -> 19.26 ms, -l 61.7 -> 60.9 ms).
 static long bwd_pix_per_block(long npix, int c, bool fused) {
-  static const long cap = getenv("YMS_BN_BWD_ROWS_CAP") ? std::max(1, atoi(getenv("YMS_BN_BWD_ROWS_CAP"))) : 256;
-  static const long cprod = getenv("YMS_BN_BWD_CCAP") ? atol(getenv("YMS_BN_BWD_CCAP")) : 32768;   // dev A/B
-  const long ccap = (fused && cprod > 0) ? std::max(32l, cprod / std::max(c, 1)) : cap;
+  constexpr long cap = 256, cprod = 32768;
+  const long ccap = fused ? std::max(32l, cprod / std::max(c, 1)) : cap;
   const long rows = std::max(1l, std::min(std::min(cap, ccap), (npix + 63) / 64));
   return (npix + rows - 1) / rows;
 }
@@ -1163,26 +1023,18 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
   const long ppb = bwd_pix_per_block(npix, c, false);
   const unsigned rows = (unsigned)((npix + ppb - 1) / ppb);
-  // software-pipelined loop (c % 8 == 0; YMS_BN_RED_PIPE=0 selects the serial loop, read per
-  // call).  At 512 rows it was step-neutral (the reduce -10%, the apply after it +5%,
-  // profiles/r03zb_bn_reduce_pipe_ab.txt); with the latency hidden inside each block, half the
-  // blocks (256 rows, bwd_pix_per_block) win: YOLOv8-s 18.63 -> 18.32 ms/step, YOLO-MS-S 37.42 ->
-  // 37.28 ms (means of four interleaved runs each, profiles/r03zd_*, r03ze_*); serial at 256
-  // rows is slower.
-  const char* pe = getenv("YMS_BN_RED_PIPE");
-  const bool pipe = !pe || atoi(pe) != 0;
-#define YMS_RED(HZ, PP)                                                                                  \
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, HZ, false, PP>), dim3(rows), dim3(256), 0, \
+  // software-pipelined loop (c % 8 == 0).  At 512 rows it was step-neutral over the serial loop
+  // (the reduce -10%, the apply after it +5%, profiles/r03zb_bn_reduce_pipe_ab.txt); with the
+  // latency hidden inside each block, half the blocks (256 rows, bwd_pix_per_block) win: YOLOv8-s
+  // 18.63 -> 18.32 ms/step, YOLO-MS-S 37.42 -> 37.28 ms (means of four interleaved runs each,
+  // profiles/r03zd_*, r03ze_*); serial at 256 rows is slower.
+#define YMS_RED(HZ)                                                                                      \
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_reduce_kernel<T, HZ, false, true>), dim3(rows), dim3(256), 0, \
                                                (hipStream_t)stream, npix, c, HZ ? (const T*)z : (const T*)nullptr, \
                                                HZ ? z_ld : 0, HZ ? z_off : 0, (const T*)gy, gy_ld, gy_off, scale,  \
                                                shift, mean_invstd, act, ws, ppb))
-  if (z) {
-    if (pipe) YMS_RED(true, true);
-    else YMS_RED(true, false);
-  } else {
-    if (pipe) YMS_RED(false, true);
-    else YMS_RED(false, false);
-  }
+  if (z) YMS_RED(true);
+  else YMS_RED(false);
 #undef YMS_RED
   return launch_status();
 }
@@ -1190,19 +1042,11 @@ yms_status yms_bn_act_bwd_reduce(int dtype, long npix, int c, const void* z, int
 yms_status yms_bn_act_bwd_finalize(int c, const float* ws, int rows, long count, float* dgamma,
                                    float* dbeta, float* coef, void* stream) {
   if (c <= 0 || !ws || rows <= 0 || count <= 0) return YMS_ERR_INVALID;
-  static const int wide = getenv("YMS_BN_FIN_1024") ? atoi(getenv("YMS_BN_FIN_1024")) : 0;   // dev A/B
-  // (tried: float4 channel quads x 32 row lanes with every load of a lane in flight at once --
-  // the step got slower, 19.42 -> 19.65 ms interleaved; the finalize is not load-latency bound)
-  static const int v2 = getenv("YMS_BN_FIN_V2") ? atoi(getenv("YMS_BN_FIN_V2")) : 0;   // dev A/B
-  if (v2)
-    hipLaunchKernelGGL(bn_bwd_finalize2_kernel, dim3(cdiv(c, 8)), dim3(256), 0, (hipStream_t)stream, c, ws, rows,
-                       count, dgamma, dbeta, coef);
-  else if (wide)
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<32>, dim3(cdiv(c, 32)), dim3(1024), 0, (hipStream_t)stream, c, ws,
-                       rows, count, dgamma, dbeta, coef);
-  else
-    hipLaunchKernelGGL(bn_bwd_finalize_kernel<8>, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, ws,
-                       rows, count, dgamma, dbeta, coef);
+  // (tried and dropped: float4 channel quads x 32 row lanes with every load of a lane in flight --
+  // 19.42 -> 19.65 ms; a latency-shaped 8-channel x 32-lane variant with 4x the blocks -- +0.15-0.3
+  // ms, profiles/r03q_bn_finalize_ab.txt: inside the step the finalize waits for CU slots, not loads)
+  hipLaunchKernelGGL(bn_bwd_finalize_kernel<8>, dim3(cdiv(c, 32)), dim3(256), 0, (hipStream_t)stream, c, ws,
+                     rows, count, dgamma, dbeta, coef);
   return launch_status();
 }
 
@@ -1217,22 +1061,13 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
   if (c > 2048) return YMS_ERR_UNSUPPORTED;
   // software-pipelined loop at eight U-pixel iterations per thread (half the blocks of the serial
   // loop's best, four): YOLO-MS-S 37.27 -> 37.11 ms/step, YOLOv8-s 18.53 -> 18.49 ms (means of
-  // two interleaved runs; 4 / 16 iterations pipelined are slower, profiles/r03zf_bn_apply_pipe_ab.txt).
-  // YMS_BN_APPLY_PIPE=0 selects the serial loop, YMS_BN_APPLY_ITERS overrides (both read per call).
-  const char* pe = getenv("YMS_BN_APPLY_PIPE");
-  const bool pipe = !pe || atoi(pe) != 0;
-  const char* ie = getenv("YMS_BN_APPLY_ITERS");
-  const int iters = ie ? std::max(1, atoi(ie)) : (pipe ? 8 : 4);
-  const long ppb = elem_ppb(npix, c, iters);
+  // two interleaved runs; 4 / 16 iterations pipelined are slower, profiles/r03zf_bn_apply_pipe_ab.txt)
+  const long ppb = elem_ppb(npix, c, 8);
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
-#define YMS_APPLY(PP)                                                                                        \
-  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, PP>), dim3(blocks), dim3(256), 0,     \
-                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,        \
-                                               (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd, coef,  \
-                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off, gres_acc, ppb))
-  if (pipe) YMS_APPLY(true);
-  else YMS_APPLY(false);
-#undef YMS_APPLY
+  YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0,
+                                               (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
+                                               (const T*)gy, gy_ld, gy_off, scale, shift, mean_invstd, coef,
+                                               act, (T*)dz, dz_ld, dz_off, (T*)gres, gres_ld, gres_off, gres_acc, ppb));
   return launch_status();
 }
 
@@ -1291,36 +1126,9 @@ yms_status yms_sppf_pool_bwd(int dtype, int n, int h, int w, int c, const void* 
   const long items = (long)n * h * w * ((c + 7) / 8);
   if (items >= (1l << 31)) return YMS_ERR_UNSUPPORTED;
   hipStream_t st = (hipStream_t)stream;
-  // whole-map fused kernel: CG channels per block so the three LDS images fit 64 KB
-  const int hw = h * w;
-  const int cg = hw <= 400 ? 32 : (hw <= 800 ? 16 : (hw <= 1600 ? 8 : 0));
-  // opt-in (YMS_SPPF_FUSED=1, read per call): bit-identical but slower inside the overlapped step,
-  // YOLOv8-s 18.37 / 18.47 -> 18.51 / 18.57 ms (profiles/r03v_sppf_fused_ab.txt): its 64 KB-LDS blocks
-  // wait for LDS the side stream's weight-gradient blocks hold
-  const int fused_on = getenv("YMS_SPPF_FUSED") ? atoi(getenv("YMS_SPPF_FUSED")) : 0;
-  if (fused_on && cg > 0 && dtype != YMS_F32) {
-    const size_t lds = (size_t)hw * cg * (2 + 2 + 1);
-    const dim3 grid((unsigned)n, (unsigned)((c + cg - 1) / cg));
-    for (int k = 3; k >= 1; --k) {
-      const int in_off = off + (k - 1) * c, gy_off = goff + k * c, gx_off = goff + (k - 1) * c;
-      if (dtype == YMS_BF16) {
-        if (cg == 32) hipLaunchKernelGGL((pool5_bwd_fused_kernel<bf16, 32>), grid, dim3(256), lds, st, h, w, c,
-                                         (const bf16*)buf, ld, in_off, (bf16*)gbuf, gy_off, gx_off);
-        else if (cg == 16) hipLaunchKernelGGL((pool5_bwd_fused_kernel<bf16, 16>), grid, dim3(256), lds, st, h, w, c,
-                                              (const bf16*)buf, ld, in_off, (bf16*)gbuf, gy_off, gx_off);
-        else hipLaunchKernelGGL((pool5_bwd_fused_kernel<bf16, 8>), grid, dim3(256), lds, st, h, w, c,
-                                (const bf16*)buf, ld, in_off, (bf16*)gbuf, gy_off, gx_off);
-      } else {
-        if (cg == 32) hipLaunchKernelGGL((pool5_bwd_fused_kernel<f16, 32>), grid, dim3(256), lds, st, h, w, c,
-                                         (const f16*)buf, ld, in_off, (f16*)gbuf, gy_off, gx_off);
-        else if (cg == 16) hipLaunchKernelGGL((pool5_bwd_fused_kernel<f16, 16>), grid, dim3(256), lds, st, h, w, c,
-                                              (const f16*)buf, ld, in_off, (f16*)gbuf, gy_off, gx_off);
-        else hipLaunchKernelGGL((pool5_bwd_fused_kernel<f16, 8>), grid, dim3(256), lds, st, h, w, c,
-                                (const f16*)buf, ld, in_off, (f16*)gbuf, gy_off, gx_off);
-      }
-    }
-    return launch_status();
-  }
+  // (round 3: a bit-identical whole-map fused backward, one launch per pool with the argmax and the
+  // gather in LDS, was slower inside the overlapped step -- 18.37-18.47 -> 18.51-18.57 ms,
+  // profiles/r03v_sppf_fused_ab.txt: its 64 KB-LDS blocks waited for the side stream's LDS)
   for (int k = 3; k >= 1; --k) {
     // pool k reads slot k-1 (value buf) and produced slot k; push grad of slot k into slot k-1
     YMS_DT_DISPATCH(dtype, T, {

@@ -1334,28 +1334,18 @@ static TileChoice choose_tile(int ncols) {
 
 static int cu_count() { return conv_cu_count(); }
 
-static int env_int(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
-// YMS_NT_VARIANT = 6 (dev A/B): 256-row tiles of 16 waves at 1 block per CU (25% fewer LDS-fill
-// bytes per FLOP, 2 k-tiles in flight).  YMS_NT_DGRAD_MULT / YMS_NT_FWD_MULT = m launch OCC x CUs x m
-// persistent blocks (dev A/B).  Read once per process.
-static int nt_variant() { static const int v = env_int("YMS_NT_VARIANT", 0); return v; }
 // forward: statistics (training) grids persistent at 1x (the side-stream wgrads hold CUs: 4x
 // measured 19.43 -> 19.9 ms/step); eval grids 4x (finer work units balance around the
-// overlapped NMS of the serving pipeline: 2.65 -> 2.58 ms/batch).  YMS_NT_FWD_MULT overrides both.
-static int nt_fwd_mult(bool stats) {
-  static const int v = env_int("YMS_NT_FWD_MULT", 0);
-  return v > 0 ? v : (stats ? 1 : 4);
-}
-static int nt_dgrad_mult() { static const int v = std::max(1, env_int("YMS_NT_DGRAD_MULT", 1 << 16)); return v; }
+// overlapped NMS of the serving pipeline: 2.65 -> 2.58 ms/batch).  (Round 4, measured and dropped:
+// 256-row tiles of 16 waves at 1 block per CU.)
+static int nt_fwd_mult(bool stats) { return stats ? 1 : 4; }
+// dgrad grids: one block per output tile (no persistent cap)
+constexpr int NT_DGRAD_MULT = 1 << 16;
 
 struct NtpGeo { int bm, bn, occ; };
 static NtpGeo ntp_geo(int cfg) {
-  const bool v6 = nt_variant() == 6;
-  if (cfg == 0) return v6 ? NtpGeo{256, 128, 1} : NtpGeo{128, 128, 2};
-  if (cfg == 1) return v6 ? NtpGeo{256, 64, 1} : NtpGeo{128, 64, 3};
+  if (cfg == 0) return NtpGeo{128, 128, 2};
+  if (cfg == 1) return NtpGeo{128, 64, 3};
   return NtpGeo{256, 32, 2};
 }
 
@@ -1384,7 +1374,7 @@ static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st)
   // the side stream, and persistent blocks that start late on CUs the wgrad kernels hold would
   // each still owe their fixed share of tiles (interleaved A/B: 19.91 -> 19.74 ms/step).
   const bool stats = EPI == EPI_STATS;
-  const long mult = MODE == MODE_FWD ? nt_fwd_mult(stats) : nt_dgrad_mult();
+  const long mult = MODE == MODE_FWD ? nt_fwd_mult(stats) : NT_DGRAD_MULT;
   const NtpGeo g = ntp_geo(cfg);
   p.tiles_n = cdiv(p.Ncols, g.bn);
   // 8-wave blocks at 2-3 per CU (4-6 waves per SIMD) hide the ds_read -> MFMA and barrier
@@ -1392,15 +1382,9 @@ static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st)
   // (round 4, measured and dropped: 256 x 128 tiles of 8 waves with 64 x 64 wave tiles, 5-40 %
   // slower, and 128 x 128 tiles of 4 such waves, within +-5 %: profiles/r04b_conv_micro_v*.txt)
   if (cfg == 0) {
-    if (g.bm == 256)
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 128, 4, 4, 3, UNI, 1, PRO>, p, 256, gy, st, g.occ * mult, 1024, stats);
-    else
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2, PRO>, p, 128, gy, st, g.occ * mult, 512, stats);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2, PRO>, p, 128, gy, st, g.occ * mult, 512, stats);
   } else if (cfg == 1) {
-    if (g.bm == 256)
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 64, 8, 2, 3, UNI, 1, PRO>, p, 256, gy, st, g.occ * mult, 1024, stats);
-    else
-      launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3, PRO>, p, 128, gy, st, g.occ * mult, 512, stats);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3, PRO>, p, 128, gy, st, g.occ * mult, 512, stats);
   } else {
     launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2, PRO>, p, 256, gy, st, g.occ * mult, 512, stats);
   }
@@ -1468,14 +1452,8 @@ static yms_status dispatch_nt(const NTParams& p, int dtype, int ks, int cfg, hip
 
 
 struct WgradPlan {
-  int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc, kp, var;
+  int bm, bn, tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld, cin8, cpt, kc, kp;
 };
-// wgrad kernel variant for 16-bit types: 0 = 32-pixel k-tiles / 4 waves, 1 = 64 / 4 waves,
-// 2 = 64 / 8 waves (1 block per CU), 3 = 32 / 8 waves.  YMS_WG_VARIANT overrides (dev A/B).
-static int wgrad_variant(int dtype) {
-  static const int v = getenv("YMS_WG_VARIANT") ? atoi(getenv("YMS_WG_VARIANT")) : 0;
-  return dtype == YMS_F32 ? 0 : v;
-}
 static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   WgradPlan w;
   const int es = elem_size(s->dtype);
@@ -1489,15 +1467,12 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   w.tiles_n = cdiv(kf, w.bn);
   w.slab_rows = w.tiles_m * w.bm;
   w.slab_ld = w.tiles_n * w.bn;
-  w.var = wgrad_variant(s->dtype);
   w.kp = 32;
   const long M = (long)s->n * s->ho * s->wo;
   w.nkt = cdiv(M, w.kp);
   const int blocks = w.tiles_m * w.tiles_n;
-  // about 4 workgroups per CU (2-4 resident by LDS), at least 512
-  // pixels per split
-  static const int wpc = getenv("YMS_WG_WPC") ? std::max(1, atoi(getenv("YMS_WG_WPC"))) : 4;
-  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(wpc * cu_count(), blocks)));
+  // about 4 workgroups per CU (2-4 resident by LDS), at least 512 pixels per split
+  int splits = std::max(1, std::min(cdiv(w.nkt, 512 / w.kp), cdiv(4 * cu_count(), blocks)));
   // deep layers: every split writes (and the reduce re-reads) a full fp32 slab of the weight
   // gradient, which can exceed the layer's own x + dz bytes several times over.  Cap the slab
   // round trip at `ratio` x the algorithmic bytes, keeping at least `min_blocks` workgroups.
@@ -1508,7 +1483,7 @@ static WgradPlan wgrad_plan(const yms_conv_shape* s) {
   // profiles/r04ad_wgrad_slab_ratio_ab.txt): fewer, longer side-stream blocks and ~no slab bytes.
   // (read per call, as the ring / halo kernels do: tests switch them at run time)
   const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;
-  const int min_blocks = getenv("YMS_WG_MIN_BLOCKS") ? std::max(1, atoi(getenv("YMS_WG_MIN_BLOCKS"))) : 256;
+  const int min_blocks = 256;
   if (ratio > 0.0) {
     const double data = (double)M * (double)(rup(s->cout, 8) + w.cin8) * es;
     const double slab_rt = 2.0 * 4.0 * (double)w.slab_rows * (double)w.slab_ld;
@@ -1541,17 +1516,10 @@ static void launch_wgrad_v(const TTParams& p, int bm, int bn, dim3 grid, hipStre
     hipLaunchKernelGGL((conv_wgrad_kernel<T, KS, 128, 128, KP, NW, OCC>), grid, dim3(NW * 64), 0, st, p);
 }
 
+// (round 3, measured and dropped: 64-pixel k-tiles, 8-wave blocks, 3-4 blocks per CU)
 template <typename T, int KS>
-static void launch_wgrad(const TTParams& p, int var, int bm, int bn, dim3 grid, hipStream_t st) {
-  if constexpr (sizeof(T) == 4) {
-    (void)var;
-    launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
-  } else {
-    if (var == 1) launch_wgrad_v<T, KS, 32, 4, 4>(p, bm, bn, grid, st);
-    else if (var == 2) launch_wgrad_v<T, KS, 32, 4, 3>(p, bm, bn, grid, st);
-    else if (var == 3) launch_wgrad_v<T, KS, 32, 8, 2>(p, bm, bn, grid, st);
-    else launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
-  }
+static void launch_wgrad(const TTParams& p, int bm, int bn, dim3 grid, hipStream_t st) {
+  launch_wgrad_v<T, KS, 32, 4, 2>(p, bm, bn, grid, st);
 }
 
 }  // namespace yms
@@ -1731,9 +1699,9 @@ yms_status yms_conv_fwd_pro(const yms_conv_shape* s, const void* z, int z_ld, in
   const TileChoice tc = choose_tile(s->cout);
   hipStream_t st = (hipStream_t)stream;
   if (s->dtype == YMS_BF16) {
-    if (s->k == 1) launch_ntp_pro<bf16, 1>(p, tc.cfg, st); else launch_ntp_pro<bf16, 3>(p, tc.cfg, st);
+    launch_ntp_pro<bf16, 1>(p, tc.cfg, st);
   } else {
-    if (s->k == 1) launch_ntp_pro<f16, 1>(p, tc.cfg, st); else launch_ntp_pro<f16, 3>(p, tc.cfg, st);
+    launch_ntp_pro<f16, 1>(p, tc.cfg, st);
   }
   return launch_status();
 }
@@ -1811,6 +1779,19 @@ size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s) {
   return (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float);
 }
 
+// fewer split-K partial slabs when the caller's workspace holds fewer than the plan asks for (a
+// workspace sized under other YMS_WG_* settings than the call's): units of work (patches / k-tiles)
+// per split grow until `splits` slabs of slab_bytes fit; false when not even one fits
+static bool fit_splits(size_t ws_bytes, size_t slab_bytes, int units, int& per, int& splits) {
+  const size_t cap = ws_bytes / slab_bytes;
+  if (cap < 1) return false;
+  if ((size_t)splits > cap) {
+    per = cdiv(units, (int)cap);
+    splits = cdiv(units, per);
+  }
+  return true;
+}
+
 yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int x_off,
                           const void* dz, int dz_ld, int dz_off, float* ws, size_t ws_bytes,
                           float* dw, int accumulate, void* stream) {
@@ -1820,7 +1801,8 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
     // 3x3: the halo-tiled kernel (wgrad_halo.hip) stages each input patch once for all nine taps
     WHPlan wh;
     if (wgrad_halo_plan(s, &wh)) {
-      if (ws_bytes < (size_t)wh.splits * wh.wk * wh.slab_rows * wh.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
+      if (!fit_splits(ws_bytes, (size_t)wh.wk * wh.slab_rows * wh.slab_ld * sizeof(float), wh.npatch, wh.pps, wh.splits))
+        return YMS_ERR_INVALID;
       yms_status e = wgrad_halo_launch(s, wh, x, x_ld, x_off, dz, dz_ld, dz_off, ws, (hipStream_t)stream);
       if (e != YMS_OK) return e;
       const int cin8 = (int)rup(s->cin, 8);
@@ -1835,7 +1817,8 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
     // 1x1 / 3x3 with > 32 output channels: both operands on an LDS-DMA ring (wgrad_ring.hip)
     WRPlan wr;
     if (wgrad_ring_plan(s, &wr)) {
-      if (ws_bytes < (size_t)wr.splits * wr.slab_rows * wr.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
+      if (!fit_splits(ws_bytes, (size_t)wr.slab_rows * wr.slab_ld * sizeof(float), wr.nkt, wr.kt_per_split, wr.splits))
+        return YMS_ERR_INVALID;
       yms_status e = wgrad_ring_launch(s, wr, x, x_ld, x_off, dz, dz_ld, dz_off, ws, (hipStream_t)stream);
       if (e != YMS_OK) return e;
       const int kf = s->k * s->k * wr.cin8;
@@ -1846,7 +1829,8 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
     }
   }
   WgradPlan w = wgrad_plan(s);
-  if (ws_bytes < (size_t)w.splits * w.slab_rows * w.slab_ld * sizeof(float)) return YMS_ERR_INVALID;
+  if (!fit_splits(ws_bytes, (size_t)w.slab_rows * w.slab_ld * sizeof(float), w.nkt, w.kt_per_split, w.splits))
+    return YMS_ERR_INVALID;
   TTParams p{};
   p.x = (const char*)x; p.dz = (const char*)dz; p.slab = ws;
   p.x_ld = x_ld; p.x_off = x_off; p.dz_ld = dz_ld; p.dz_off = dz_off;
@@ -1869,11 +1853,11 @@ yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int 
   p.tiles_m_n = w.tiles_m * w.tiles_n;
   dim3 grid((unsigned)(w.tiles_m * w.tiles_n * w.splits));
   if (s->dtype == YMS_BF16) {
-    if (s->k == 1) launch_wgrad<bf16, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<bf16, 3>(p, w.var, w.bm, w.bn, grid, st);
+    if (s->k == 1) launch_wgrad<bf16, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<bf16, 3>(p, w.bm, w.bn, grid, st);
   } else if (s->dtype == YMS_F16) {
-    if (s->k == 1) launch_wgrad<f16, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<f16, 3>(p, w.var, w.bm, w.bn, grid, st);
+    if (s->k == 1) launch_wgrad<f16, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<f16, 3>(p, w.bm, w.bn, grid, st);
   } else {
-    if (s->k == 1) launch_wgrad<float, 1>(p, w.var, w.bm, w.bn, grid, st); else launch_wgrad<float, 3>(p, w.var, w.bm, w.bn, grid, st);
+    if (s->k == 1) launch_wgrad<float, 1>(p, w.bm, w.bn, grid, st); else launch_wgrad<float, 3>(p, w.bm, w.bn, grid, st);
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;

@@ -24,13 +24,7 @@
 namespace yms {
 
 constexpr int DW_TY = 8, DW_TX = 32, DW_RX = 4, DW_G = 4, DW_CB = DW_G * 8;   // 32 channels per block
-// DW_DGRAD_RED: dgrad whose output (the producer's activation gradient, sole writer) also feeds
-// the producer's BN + SiLU backward statistics: the fused pass reads the producer's z once per
-// output pixel and writes one partial row per strip -- the separate reduce pass re-read dx and z
-// DW_FWD_STATS_BNIN: the training forward whose input x = act(BN(z)) of the producer is not
-// materialised: the producer's z rows land in the ring and are converted in LDS once per element
-// (zero padding stays zero) -- the producer's affine_act pass (read z, write x) goes
-enum { DW_FWD_AFFINE = 0, DW_FWD_STATS = 1, DW_DGRAD = 2, DW_DGRAD_RED = 3, DW_FWD_STATS_BNIN = 4 };
+enum { DW_FWD_AFFINE = 0, DW_FWD_STATS = 1, DW_DGRAD = 2 };
 
 struct DwParams {
   const char* src;
@@ -48,57 +42,7 @@ struct DwParams {
   int N, H, W, C;
   int tiles_x, tiles_y;  // spatial tiles per image
   int ysplit, tps;       // forward / dgrad: strips per image column of tiles, tiles per strip
-  int waitall;
-  // DW_DGRAD_RED: the producer's pre-BN z (same pixels / channels as dx), its BN scale / shift /
-  // (mean, invstd), activation, and the partial rows [strip][2][C] (bn_bwd_reduce_kernel layout)
-  const char* rz;
-  int rz_ld, rz_off;
-  const float *rsc, *rsh, *rmi;
-  int ract;
-  float* rws;
-  // DW_FWD_STATS_BNIN / wgrad with an input affine: x = act(src * isc + ish) per channel
-  const float *isc, *ish;
-  int iact;
 };
-
-// per-element input transform of a staged chunk (the producer's affine_act formula)
-template <typename T>
-__device__ __forceinline__ void dw_in_affine(Raw8<T>& r, const float (&sc)[8], const float (&sh)[8], int act) {
-  float v[8];
-  unpack8(r, v);
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    float a = v[k] * sc[k] + sh[k];
-    if (act == YMS_ACT_SILU) a = silu_f(a);
-    v[k] = a;
-  }
-  T t[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) t[k] = (T)v[k];
-  __builtin_memcpy(&r, t, sizeof(t));
-}
-// convert rows [yfirst, yfirst + nrows) of a wave's ring in place (valid pixels only: the padding
-// the DMA zero-filled must stay zero, not act(shift)); wave-local, ends with the LDS writes done
-template <typename T, int K, int HW, int RB, int RS>
-__device__ __forceinline__ void dw_ring_in_affine(Raw8<T>* wring, int yfirst, int nrows, int x0, int H, int W,
-                                                  bool cok, const float (&sc)[8], const float (&sh)[8], int act,
-                                                  int lane) {
-  constexpr int P = K / 2;
-  if (cok) {
-    for (int j = lane; j < nrows * HW; j += 64) {
-      const int r = j / HW, col = j - r * HW;
-      const int y = yfirst + r, x = x0 - P + col;
-      if (y >= 0 && y < H && x >= 0 && x < W) {
-        Raw8<T>* cp = wring + ((y + P) % RB) * RS + col;
-        Raw8<T> v = *cp;
-        dw_in_affine<T>(v, sc, sh, act);
-        *cp = v;
-      }
-    }
-  }
-  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): this wave's LDS writes are done
-  __builtin_amdgcn_wave_barrier();
-}
 
 // LDS row stride (16-B chunks) for rows of n chunks: one chunk of padding when n is a multiple
 // of 4 (a 64-B multiple: rows read by one wave's lanes would start in the same banks); other
@@ -107,7 +51,7 @@ constexpr int dw_rs(int n) { return n % 4 == 0 ? n + 1 : n; }
 
 // stage the (TY + K - 1) x (TX + K - 1) halo of 32 channels (zero outside the image / past C)
 // into rows of dw_rs(HW) chunks
-template <typename T, int K, int NT = 256, bool BNIN = false>
+template <typename T, int K, int NT = 256>
 __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, int n, int y0, int x0, int c0) {
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1, P = K / 2, RS = dw_rs(HW);
   const T* src = reinterpret_cast<const T*>(p.src);
@@ -118,18 +62,8 @@ __device__ __forceinline__ void dw_stage_halo(const DwParams& p, Raw8<T>* lds, i
     Raw8<T> v;
 #pragma unroll
     for (int k = 0; k < (int)(sizeof(T) / 2); ++k) v.v[k] = u32x4{0u, 0u, 0u, 0u};
-    if (y >= 0 && y < p.H && x >= 0 && x < p.W && c < p.C) {
+    if (y >= 0 && y < p.H && x >= 0 && x < p.W && c < p.C)
       load_raw8(src + (((long)n * p.H + y) * p.W + x) * p.src_ld + p.src_off + c, min(8, p.C - c), v);
-      if constexpr (BNIN) {
-        float sc[8], sh[8];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          sc[k] = c + k < p.C ? p.isc[c + k] : 0.f;
-          sh[k] = c + k < p.C ? p.ish[c + k] : 0.f;
-        }
-        dw_in_affine<T>(v, sc, sh, p.iact);
-      }
-    }
     lds[(g * HH + hy) * RS + hx] = v;
   }
 }
@@ -212,8 +146,7 @@ __device__ __forceinline__ Raw8<T> pack_raw8(const float (&v)[8]) {
 }
 
 template <typename T, int K, int MODE, int TX = DW_TX, int G = DW_G>
-__global__ __launch_bounds__(G * 64, (MODE == 3 ? (G == 8 ? 1 : (sizeof(T) == 4 && K > 3 ? 1 : 2))
-                                                 : (G == 8 ? 2 : DwOcc<T, K>::v)))
+__global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v))
 void dwconv_kernel(DwParams p) {
   constexpr int CB = G * 8, NT = G * 64;
   constexpr int TY = DwTy<TX>::v, CGX = TX / DW_RX;
@@ -223,12 +156,8 @@ void dwconv_kernel(DwParams p) {
   constexpr int RS = dw_rs(HW);   // ring row stride (chunks)
   constexpr int RING_B = G * RB * RS * (int)sizeof(Raw8<T>);
   constexpr int WL_B = G * K * K * 8 * (int)sizeof(float);
-  constexpr bool RED = MODE == DW_DGRAD_RED;
-  constexpr bool BNIN = MODE == DW_FWD_STATS_BNIN;
-  constexpr bool STATS = MODE == DW_FWD_STATS || BNIN;
-  constexpr int RP_B = RED ? G * 4 * 8 * (int)sizeof(float) : 0;
-  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + G * 16 * (int)sizeof(float) + RP_B];
-  float (*rpar)[4][8] = reinterpret_cast<float (*)[4][8]>(smem + RING_B + WL_B + G * 16 * (int)sizeof(float));
+  constexpr bool STATS = MODE == DW_FWD_STATS;
+  __shared__ __attribute__((aligned(16))) char smem[RING_B + WL_B + G * 16 * (int)sizeof(float)];
   Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
   float (*wl)[K * K][8] = reinterpret_cast<float (*)[K * K][8]>(smem + RING_B);
   float (*scl)[16] = reinterpret_cast<float (*)[16]>(smem + RING_B + WL_B);   // eval scale | shift (LDS:
@@ -254,7 +183,7 @@ void dwconv_kernel(DwParams p) {
       const int it = threadIdx.x + NT * j;
       if (it < CB * K * K) {
         const int cl = it / (K * K), t = it - cl * (K * K);
-        const int tw = (MODE == DW_DGRAD || MODE == DW_DGRAD_RED) ? K * K - 1 - t : t;
+        const int tw = MODE == DW_DGRAD ? K * K - 1 - t : t;
         wl[cl >> 3][tw][cl & 7] = wv[j];
       }
     }
@@ -264,41 +193,9 @@ void dwconv_kernel(DwParams p) {
     scl[gg][threadIdx.x & 15] = (threadIdx.x & 8) ? ((p.shift && c < p.C) ? p.shift[c] : 0.0f)
                                                   : ((p.scale && c < p.C) ? p.scale[c] : 1.0f);
   }
-  if (RED && threadIdx.x < G * 32) {
-    // the producer's BN scale, shift, mean, invstd of the block's channels (LDS: not live across
-    // the FMAs)
-    const int gg = threadIdx.x >> 5, j = (threadIdx.x >> 3) & 3, k = threadIdx.x & 7, cc = c0 + 8 * gg + k;
-    const float* src = j == 0 ? p.rsc : (j == 1 ? p.rsh : (j == 2 ? p.rmi : p.rmi + p.C));
-    rpar[gg][j][k] = cc < p.C ? src[cc] : 0.0f;
-  }
   const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ty = lane / CGX, qx = lane - ty * CGX;   // ty >= TY: idle lane (60 of 64 used at TX 20 / 40)
   const int c = c0 + 8 * g, nv = min(8, p.C - c);
-  // DW_DGRAD_RED: this lane's RX chunks of the producer's z for tile t (prefetched a tile ahead)
-  // and its running (sum da, sum da * xhat) over the strip
-  const T* rzp = RED ? reinterpret_cast<const T*>(p.rz) + (long)n * p.H * p.W * p.rz_ld + p.rz_off : nullptr;
-  auto load_rz = [&](int t, Raw8<T> (&d)[DW_RX]) {
-    const int y = t * TY + ty;
-#pragma unroll
-    for (int i = 0; i < DW_RX; ++i) {
-      const int x = x0 + 4 * qx + i;
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) d[i].v[k] = u32x4{0u, 0u, 0u, 0u};
-      if (ty < TY && y < p.H && x < p.W && nv > 0) load_raw8(rzp + ((long)y * p.W + x) * p.rz_ld + c, 8, d[i]);
-    }
-  };
-  float isc[8], ish[8];
-  if constexpr (BNIN) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      isc[k] = c + k < p.C ? p.isc[c + k] : 0.f;
-      ish[k] = c + k < p.C ? p.ish[c + k] : 0.f;
-    }
-  }
-  Raw8<T> rzc[RED ? DW_RX : 1], rzn[RED ? DW_RX : 1];
-  float ra1[8], ra2[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) { ra1[k] = 0.f; ra2[k] = 0.f; }
   // raw buffer resource over image n's rows (32-bit offsets: checked on the host)
   const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
                                                    (long)n * p.H * p.W * p.src_ld + p.src_off);
@@ -322,19 +219,11 @@ void dwconv_kernel(DwParams p) {
   for (int hy = 0; hy < TY + K - 1; ++hy)
     dw_row_dma<T, K, TX>(rs, myring + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
                          p.src_ld, lane);
-  if constexpr (RED) load_rz(t0, rzc);
   wait_vmcnt<0>();
   __syncthreads();
   for (int t = t0; t < t1; ++t) {
     const int y0 = t * TY;
     const bool more = t + 1 < t1;
-    if constexpr (BNIN) {
-      // the rows that landed for this tile (all TY + K - 1 of the strip's first tile)
-      if (t == t0) dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 - P, TY + K - 1, x0, p.H, p.W, nv > 0,
-                                                       isc, ish, p.iact, lane);
-      else dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 + P, TY, x0, p.H, p.W, nv > 0, isc, ish,
-                                               p.iact, lane);
-    }
     // the next tile's TY new rows y0 + TY + P .. y0 + 2 TY - 1 + P go to slots this tile does not read
     if (more) {
       int sl = (y0 + TY + 2 * P) % RB;
@@ -342,7 +231,6 @@ void dwconv_kernel(DwParams p) {
         dw_row_dma<T, K, TX>(rs, myring + sl * ROWB, y0 + TY + P + hy, x0, c, p.H, p.W, p.C, p.src_ld, lane);
         sl = sl + 1 == RB ? 0 : sl + 1;
       }
-      if constexpr (RED) load_rz(t + 1, rzn);
     }
     const Raw8<T>* hp = ring + g * RB * RS + 4 * (ty < TY ? qx : 0);
     float acc[DW_RX][8];
@@ -411,21 +299,6 @@ void dwconv_kernel(DwParams p) {
 #pragma unroll
       for (int h = 0; h < (int)(sizeof(T) / 2); ++h)
         dw_bst16(rd, ok ? e * (uint32_t)sizeof(T) + 16u * h : NT_OOB, rv.v[h]);
-      if constexpr (RED) {
-        // the producer's BN + SiLU backward sums on dx as stored (bn_bwd_reduce_kernel's formula);
-        // out-of-image / idle lanes have z = 0 and dx = 0 chunks -- masked by ok
-        float gq[8], zv[8];
-        unpack8(rv, gq);
-        unpack8(rzc[i], zv);
-#pragma unroll
-        for (int k = 0; k < 8; ++k) {
-          const float a = zv[k] * rpar[g][0][k] + rpar[g][1][k];
-          const float da = p.ract == YMS_ACT_SILU ? gq[k] * dsilu_f(a) : gq[k];
-          const float xh = (zv[k] - rpar[g][2][k]) * rpar[g][3][k];
-          ra1[k] += ok ? da : 0.0f;
-          ra2[k] += ok ? da * xh : 0.0f;
-        }
-      }
     }
     if (STATS) {
       // one statistics row per spatial tile (conv_common.hpp contract; its pixel count goes to the
@@ -469,35 +342,8 @@ void dwconv_kernel(DwParams p) {
       dw_bst4(rstat, sok ? so + (uint32_t)p.stats_ld * 4u : NT_OOB, b);
       dw_bst4(rcnt, (blockIdx.y == 0 && threadIdx.x == 0) ? (uint32_t)tile * 4u : NT_OOB, (float)(vy * vx));
     }
-    if (!p.waitall) wait_vmcnt<NST>();
-    else wait_vmcnt<0>();   // dev A/B (YMS_DW_WAITALL=1): also drain the tile's stores
+    wait_vmcnt<NST>();
     __syncthreads();
-    if constexpr (RED) {
-      if (more) {
-#pragma unroll
-        for (int i = 0; i < DW_RX; ++i) rzc[i] = rzn[i];
-      }
-    }
-  }
-  if constexpr (RED) {
-    // fixed-order butterfly over the wave's lanes; lanes 0..7 write channel c + lane of the strip's
-    // partial row blockIdx.x (every strip covers all channels through blockIdx.y)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) {
-        ra1[k] += __shfl_xor(ra1[k], m);
-        ra2[k] += __shfl_xor(ra2[k], m);
-      }
-    }
-    float a = 0.f, b = 0.f;
-#pragma unroll
-    for (int k = 0; k < 8; ++k)
-      if (k == lane) { a = ra1[k]; b = ra2[k]; }
-    if (lane < 8 && c + lane < p.C) {
-      p.rws[(long)blockIdx.x * 2 * p.C + c + lane] = a;
-      p.rws[(long)blockIdx.x * 2 * p.C + p.C + c + lane] = b;
-    }
   }
 }
 
@@ -516,7 +362,7 @@ struct DwWg {
 };
 constexpr int DW_WG_NT = 512, DW_WG_LPG = DW_WG_NT / DW_G;
 
-template <typename T, int K, bool BNIN = false>
+template <typename T, int K>
 __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
                                                                  float* ws) {
   constexpr int HH = DW_TY + K - 1, HW = DW_TX + K - 1;
@@ -548,7 +394,7 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
     const int n = tile / per_img, rem = tile - n * per_img;
     const int y0 = (rem / p.tiles_x) * DW_TY, x0 = (rem % p.tiles_x) * DW_TX;
     __syncthreads();      // previous tile's LDS reads are done
-    dw_stage_halo<T, K, DW_WG_NT, BNIN>(p, halo, n, y0, x0, c0);
+    dw_stage_halo<T, K, DW_WG_NT>(p, halo, n, y0, x0, c0);
     for (int it = threadIdx.x; it < DZN; it += DW_WG_NT) {
       const int g2 = it / (DW_TY * DW_TX), r2 = it - g2 * (DW_TY * DW_TX);
       const int y = y0 + r2 / DW_TX, x = x0 + r2 % DW_TX, c = c0 + 8 * g2;
@@ -607,7 +453,7 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad_kernel(DwParams p, cons
   }
 }
 
-// wgrad, k = 5 / 7 / 9, 16-bit types (default; YMS_DW_WG2=0 keeps the kernel above): the same lane
+// wgrad, k = 5 / 7 / 9, 16-bit types (fp32 keeps the kernel above): the same lane
 // work as dwconv_wgrad_kernel -- lane (dy, ty, s) of a channel group keeps the K x 8 partial taps of
 // kernel row dy for its tile row and column segment in registers across all of the block's tiles --
 // on tiles shaped for the map and the kernel: TX = the forward's width (20 / 40 / 32: no idle
@@ -757,7 +603,7 @@ __global__ __launch_bounds__(DW_WG_NT) void dwconv_wgrad2_kernel(DwParams p, con
 // chunks.  At the end the 72 partials are summed over the wave's lanes by a fixed butterfly and
 // lane 0 writes ws[block][tap][c] (dwconv_wgrad_reduce_kernel sums the strips in a fixed order).
 // Replaces the 8 x 32-tile kernel above for k = 3, which staged each tile synchronously.
-template <typename T, int TX, int G, bool BNIN = false>
+template <typename T, int TX, int G>
 __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, const char* dz, int dz_ld, int dz_off,
                                                                   float* ws) {
   constexpr int K = 3, P = 1;
@@ -800,14 +646,6 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
     for (int b = 0; b < K; ++b)
 #pragma unroll
       for (int k = 0; k < 8; ++k) part[a][b][k] = 0.0f;
-  float isc[8], ish[8];
-  if constexpr (BNIN) {
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      isc[k] = c + k < p.C ? p.isc[c + k] : 0.f;
-      ish[k] = c + k < p.C ? p.ish[c + k] : 0.f;
-    }
-  }
   Raw8<T> dzc[DW_RX], dzn[DW_RX];
   for (int hy = 0; hy < TY + K - 1; ++hy)
     dw_row_dma<T, K, TX>(rs, myring + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
@@ -819,12 +657,6 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
   for (int t = t0; t < t1; ++t) {
     const int y0 = t * TY;
     const bool more = t + 1 < t1;
-    if constexpr (BNIN) {
-      if (t == t0) dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 - P, TY + K - 1, x0, p.H, p.W, nv > 0,
-                                                       isc, ish, p.iact, lane);
-      else dw_ring_in_affine<T, K, HW, RB, RS>(ring + g * RB * RS, y0 + P, TY, x0, p.H, p.W, nv > 0, isc, ish,
-                                               p.iact, lane);
-    }
     if (more) {
       int sl = (y0 + TY + 2 * P) % RB;
       for (int hy = 0; hy < TY; ++hy) {
@@ -888,112 +720,6 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
   }
 }
 
-// wgrad, k = 5 / 7 / 9: the strip walker with the kernel rows spread over the waves -- a block of K
-// waves owns 8 channels, wave dy accumulates the K x 8 partial taps of kernel row dy for the
-// RX = 4 pixels of each lane (K x 8 registers instead of K x K x 8).  The input rows (8 channels)
-// sit in one LDS-DMA ring shared by the K waves (row hy loaded by wave hy % K), the next tile's
-// rows and the lanes' dz chunks in flight while the current tile computes; fixed-order butterfly
-// per wave, ws[strip][dy K + dx][c] partial rows, dwconv_wgrad_reduce_kernel sums the strips.
-// (Opt-in, see dw_wgk: the 8 x 32-tile kernel stays the default for k >= 5.)
-template <int K> struct DwWgkOcc { static constexpr int v = K == 5 ? 3 : (K == 7 ? 2 : 1); };
-template <typename T, int K, int TX>
-__global__ __launch_bounds__(K * 64, DwWgkOcc<K>::v) void dwconv_wgradk_kernel(DwParams p, const char* dz, int dz_ld,
-                                                                              int dz_off, float* ws) {
-  constexpr int P = K / 2, TY = DwTy<TX>::v, CGX = TX / DW_RX;
-  constexpr int HW = TX + K - 1, RB = 2 * TY + K - 1, RS = dw_rs(HW);
-  __shared__ __attribute__((aligned(16))) char smem[RB * RS * (int)sizeof(Raw8<T>)];
-  Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
-  const int per_img = p.tiles_x * p.ysplit;
-  const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
-  const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
-  const int x0 = tx * TX;
-  const int c = blockIdx.y * 8, nv = min(8, p.C - c);
-  const int dy = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int wv = __builtin_amdgcn_readfirstlane(dy);
-  const int ty = lane / CGX, qx = lane - ty * CGX;
-  const uintptr_t ib = reinterpret_cast<uintptr_t>(reinterpret_cast<const T*>(p.src) +
-                                                   (long)n * p.H * p.W * p.src_ld + p.src_off);
-  const i32x4 rs = {(int)(uint32_t)ib, (int)(uint32_t)(ib >> 32) & 0xffff,
-                    (int)((long)p.H * p.W * p.src_ld * (long)sizeof(T)), NT_RSRC3};
-  const uint32_t ring0 = __builtin_amdgcn_readfirstlane((uint32_t)reinterpret_cast<uintptr_t>(ring));
-  constexpr uint32_t ROWB = RS * (uint32_t)sizeof(Raw8<T>);
-  const T* dzp = reinterpret_cast<const T*>(dz) + (long)n * p.H * p.W * dz_ld + dz_off;
-  auto load_dz = [&](int t, Raw8<T> (&d)[DW_RX]) {
-    const int y = t * TY + ty;
-#pragma unroll
-    for (int i = 0; i < DW_RX; ++i) {
-      const int x = x0 + 4 * qx + i;
-#pragma unroll
-      for (int k = 0; k < (int)(sizeof(T) / 2); ++k) d[i].v[k] = u32x4{0u, 0u, 0u, 0u};
-      if (ty < TY && y < p.H && x < p.W && nv > 0) load_raw8(dzp + ((long)y * p.W + x) * dz_ld + c, 8, d[i]);
-    }
-  };
-  float part[K][8];
-#pragma unroll
-  for (int b = 0; b < K; ++b)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) part[b][k] = 0.0f;
-  Raw8<T> dzc[DW_RX], dzn[DW_RX];
-  for (int hy = wv; hy < TY + K - 1; hy += K)
-    dw_row_dma<T, K, TX>(rs, ring0 + ((t0 * TY + hy) % RB) * ROWB, t0 * TY - P + hy, x0, c, p.H, p.W, p.C,
-                         p.src_ld, lane);
-  load_dz(t0, dzc);
-  wait_vmcnt<0>();
-  __syncthreads();
-  const Raw8<T>* hp = ring + 4 * (ty < TY ? qx : 0);
-  for (int t = t0; t < t1; ++t) {
-    const int y0 = t * TY;
-    const bool more = t + 1 < t1;
-    if (more) {
-      for (int hy = wv; hy < TY; hy += K)
-        dw_row_dma<T, K, TX>(rs, ring0 + ((y0 + TY + 2 * P + hy) % RB) * ROWB, y0 + TY + P + hy, x0, c, p.H, p.W,
-                             p.C, p.src_ld, lane);
-      load_dz(t + 1, dzn);
-    }
-    float d[DW_RX][8];
-#pragma unroll
-    for (int i = 0; i < DW_RX; ++i) unpack8(dzc[i], d[i]);
-    // input row y0 + ty + dy - P (idle lanes: row 0's, their dz is zero)
-    const Raw8<T>* row = hp + ((y0 + (ty < TY ? ty : 0) + dy) % RB) * RS;
-#pragma unroll
-    for (int q = 0; q < DW_RX + K - 1; ++q) {
-      float v[8];
-      unpack8(row[q], v);
-#pragma unroll
-      for (int i = 0; i < DW_RX; ++i) {
-        const int dx = q - i;
-        if (dx >= 0 && dx < K) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) part[dx][k] += v[k] * d[i][k];
-        }
-      }
-    }
-    wait_vmcnt<0>();
-    __syncthreads();
-    if (more) {
-#pragma unroll
-      for (int i = 0; i < DW_RX; ++i) dzc[i] = dzn[i];
-    }
-  }
-#pragma unroll
-  for (int b = 0; b < K; ++b)
-#pragma unroll
-    for (int k = 0; k < 8; ++k) {
-      float v = part[b][k];
-#pragma unroll
-      for (int m = 32; m >= 1; m >>= 1) v += __shfl_xor(v, m);
-      part[b][k] = v;
-    }
-  if (lane == 0 && nv > 0) {
-#pragma unroll
-    for (int b = 0; b < K; ++b) {
-      float* o = ws + ((long)blockIdx.x * K * K + dy * K + b) * p.C + c;
-      *reinterpret_cast<f32x4*>(o) = f32x4{part[b][0], part[b][1], part[b][2], part[b][3]};
-      *reinterpret_cast<f32x4*>(o + 4) = f32x4{part[b][4], part[b][5], part[b][6], part[b][7]};
-    }
-  }
-}
-
 // dw[c][t] (+)= sum_b ws[b][t][c]: 64 outputs per block, 16 waves; wave w sums blocks
 // b = w (mod 16) into 4 independent partials (4 loads in flight per lane; one dependent chain
 // over ~500 rows made the reduce latency-bound), then a fixed-order tree over the waves
@@ -1034,15 +760,9 @@ static int dw_tiles(const yms_dw_shape* s, int& tx, int& ty) {
   return s->n * tx * ty;
 }
 
-static int dw_env(const char* name, int dflt) {
-  const char* v = getenv(name);
-  return v ? atoi(v) : dflt;
-}
 // forward / dgrad tile width (DwTy): whole tiles across the 20 / 40 / 80-wide maps of a 640 input,
-// 32 where it divides the width (YMS_DW_TX=32|40|20 forces one: dev A/B, read per call)
+// 32 where it divides the width
 static int dw_fwd_tx(const yms_dw_shape* s) {
-  const int f = dw_env("YMS_DW_TX", 0);
-  if (f == 32 || f == 40 || f == 20) return f;
   if (s->w % 32 == 0) return 32;
   if (s->w % 40 == 0) return 40;
   if (s->w <= 20) return 20;
@@ -1063,42 +783,29 @@ static int dw_occ(const yms_dw_shape* s) {
 
 // channel groups of 8 per forward / dgrad block: 8 (64 channels = one 128-B line of an NHWC pixel
 // per block, 512 threads) for k = 3 when C is a multiple of 64, else 4 (32 channels: the other half
-// of each line is read and written by another block at another time).  YMS_DW_G=4|8 forces (dev A/B).
-static int dw_fwd_g(const yms_dw_shape* s) {
-  const bool g8_ok = s->k == 3 && s->c % 64 == 0 && s->dtype != YMS_F32;
-  const int f = dw_env("YMS_DW_G", 0);
-  if (f == 4 || (f == 8 && g8_ok)) return f;   // the override never lifts the G = 8 path's conditions
-  return g8_ok ? 8 : 4;
-}
+// of each line is read and written by another block at another time).
+static int dw_fwd_g(const yms_dw_shape* s) { return s->k == 3 && s->c % 64 == 0 && s->dtype != YMS_F32 ? 8 : 4; }
 
 // forward / dgrad grid: image column tiles split into strips of tps tiles.  The strip length is
 // chosen so the blocks fill whole rounds of the resident slots (occupancy x CUs): a block walks its
 // strip serially, so a last round of a few blocks costs a full strip time, while shorter strips
-// re-read K - 1 halo rows each (cost model: rounds x (tps TY + K - 1) rows).  YMS_DW_BLOCKS=n
-// restores the earlier rule (strips split until about n blocks).
+// re-read K - 1 halo rows each (cost model: rounds x (tps TY + K - 1) rows).
 static dim3 dw_strip_grid(const yms_dw_shape* s, DwParams& p) {
   dw_fwd_tiles(s, p.tiles_x, p.tiles_y);
   const int TY = dw_fwd_ty(dw_fwd_tx(s)), G = dw_fwd_g(s);
   const long cg = (s->c + 8 * G - 1) / (8 * G);
   const long base = (long)s->n * p.tiles_x * cg;
-  const long target = dw_env("YMS_DW_BLOCKS", 0);
-  if (target > 0) {
-    const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (target + base - 1) / base));
-    p.tps = (p.tiles_y + want - 1) / want;
-  } else {
-    const long slots = (long)(G == 8 ? 2 : dw_occ(s)) * conv_cu_count();
-    double best = 1e30;
-    int best_tps = p.tiles_y;
-    for (int tps = p.tiles_y; tps >= 1; --tps) {
-      const long ys = (p.tiles_y + tps - 1) / tps;
-      const long rounds = (base * ys + slots - 1) / slots;
-      const double cost = (double)rounds * (tps * TY + s->k - 1);
-      if (cost < best * 0.999) { best = cost; best_tps = tps; }
-    }
-    p.tps = best_tps;
+  const long slots = (long)(G == 8 ? 2 : dw_occ(s)) * conv_cu_count();
+  double best = 1e30;
+  int best_tps = p.tiles_y;
+  for (int tps = p.tiles_y; tps >= 1; --tps) {
+    const long ys = (p.tiles_y + tps - 1) / tps;
+    const long rounds = (base * ys + slots - 1) / slots;
+    const double cost = (double)rounds * (tps * TY + s->k - 1);
+    if (cost < best * 0.999) { best = cost; best_tps = tps; }
   }
+  p.tps = best_tps;
   p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
-  p.waitall = dw_env("YMS_DW_WAITALL", 0);
   return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
 }
 
@@ -1114,19 +821,17 @@ static bool dw_image_fits(const yms_dw_shape* s, int ld) {
   return (long)s->h * s->w * ld * esz < (long)NT_OOB;
 }
 
-// k = 3 weight gradient on the strip walker (16-bit; YMS_DW_WG3=0 keeps the tile kernel: dev A/B)
-static bool dw_wg3(const yms_dw_shape* s) { return s->k == 3 && s->dtype != YMS_F32 && dw_env("YMS_DW_WG3", 1) != 0; }
-// its grid: the forward's tiles and channel blocks; strips as long as whole rounds of the resident
-// blocks allow (cost model as dw_strip_grid, plus the per-strip butterfly and partial row ~ 3 tiles)
-// channel groups per wgrad block: 4 by default (two 256-thread blocks per CU at ~230 VGPRs);
-// YMS_DW_WG3_G=8 uses the forward's 64-channel blocks where they apply (dev A/B)
-static int dw_wg3_g(const yms_dw_shape* s) { return dw_env("YMS_DW_WG3_G", 4) == 8 ? dw_fwd_g(s) : 4; }
+// k = 3 weight gradient on the strip walker (16-bit types; fp32 keeps the tile kernel)
+static bool dw_wg3(const yms_dw_shape* s) { return s->k == 3 && s->dtype != YMS_F32; }
+// its grid: the forward's tiles, 32-channel blocks (two 256-thread blocks per CU at ~230 VGPRs);
+// strips as long as whole rounds of the resident blocks allow (cost model as dw_strip_grid, plus
+// the per-strip butterfly and partial row ~ 3 tiles)
 static dim3 dw_wg3_grid(const yms_dw_shape* s, DwParams& p) {
   dw_fwd_tiles(s, p.tiles_x, p.tiles_y);
-  const int TY = dw_fwd_ty(dw_fwd_tx(s)), G = dw_wg3_g(s);
-  const long cg = (s->c + 8 * G - 1) / (8 * G);
+  const int TY = dw_fwd_ty(dw_fwd_tx(s));
+  const long cg = (s->c + 31) / 32;
   const long base = (long)s->n * p.tiles_x * cg;
-  const long slots = (G == 8 ? 1l : 2l) * conv_cu_count();
+  const long slots = 2l * conv_cu_count();
   double best = 1e30;
   int best_tps = p.tiles_y;
   for (int tps = p.tiles_y; tps >= 1; --tps) {
@@ -1140,31 +845,8 @@ static dim3 dw_wg3_grid(const yms_dw_shape* s, DwParams& p) {
   return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
 }
 
-// k = 5 / 7 / 9 weight gradient with the kernel rows over the waves: opt-in (YMS_DW_WGK=1), measured
-// no better than the tile kernel at B = 64 (k5@80 c128 184 -> 202 us, k7@40 c256 149 -> 138 us,
-// k9@20 c512 138 -> 320 us: 8-channel blocks read 16 B per pixel line, and k = 9 spills at one
-// 9-wave block per CU; profiles/r03n_dw_wgradk_micro.txt).  Its grid: strips x 8-channel groups.
-static bool dw_wgk(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32 && dw_env("YMS_DW_WGK", 0) == 1; }
-static dim3 dw_wgk_grid(const yms_dw_shape* s, DwParams& p) {
-  dw_fwd_tiles(s, p.tiles_x, p.tiles_y);
-  const int TY = dw_fwd_ty(dw_fwd_tx(s));
-  const long cg = (s->c + 7) / 8;
-  const long base = (long)s->n * p.tiles_x * cg;
-  const long slots = (long)(s->k == 5 ? 3 : (s->k == 7 ? 2 : 1)) * conv_cu_count();
-  double best = 1e30;
-  int best_tps = p.tiles_y;
-  for (int tps = p.tiles_y; tps >= 1; --tps) {
-    const long ys = (p.tiles_y + tps - 1) / tps;
-    const long rounds = (base * ys + slots - 1) / slots;
-    const double cost = (double)rounds * (tps * TY + s->k - 1 + 2 * TY);
-    if (cost < best * 0.999) { best = cost; best_tps = tps; }
-  }
-  p.tps = best_tps;
-  p.ysplit = (p.tiles_y + p.tps - 1) / p.tps;
-  return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
-}
-
-static bool dw_wg2(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32 && dw_env("YMS_DW_WG2", 1) != 0; }
+// k = 5 / 7 / 9 weight gradient on map-shaped tiles with register prefetch (16-bit types)
+static bool dw_wg2(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32; }
 static void dw_wg2_tile(const yms_dw_shape* s, int& tx, int& ty) {
   tx = dw_fwd_tx(s);    // DwWg2<K, TX>::TY
   ty = tx == 20 ? (s->k == 5 ? 20 : 10) : (s->k == 5 ? 12 : (s->k == 7 ? 9 : 7));
@@ -1213,104 +895,46 @@ static int dw_wgrad_blocks(const yms_dw_shape* s) {
   } while (0)
 
 // y (+)= a + b over npix x c (b may be NULL): the MS-Block branch sum (X_i + Y_{i-1}) and, with
-// b = NULL, its backward (each addend's gradient (+)= the sum's gradient).  U = 16-B items per
-// thread, all loads issued before the first store (U = 0: grid-stride loop, one item at a time).
-template <typename T, int U>
+// b = NULL, its backward (each addend's gradient (+)= the sum's gradient); grid-stride over 16-B items
+template <typename T>
 __global__ __launch_bounds__(256) void add_views_kernel(long items, int cg, const T* a, int a_ld, int a_off,
                                                         const T* b, int b_ld, int b_off, T* y, int y_ld, int y_off,
                                                         int accumulate) {
-  if constexpr (U == 0) {
-    for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
-      const long pix = it / cg;
-      const int c = (int)(it - pix * cg) * 8;
-      float va[8], vb[8], vy[8];
-      Vec8<T>::load(a + pix * a_ld + a_off + c, va);
-      if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb);
-      if (accumulate) Vec8<T>::load(y + pix * y_ld + y_off + c, vy);
+  for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
+    const long pix = it / cg;
+    const int c = (int)(it - pix * cg) * 8;
+    float va[8], vb[8], vy[8];
+    Vec8<T>::load(a + pix * a_ld + a_off + c, va);
+    if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb);
+    if (accumulate) Vec8<T>::load(y + pix * y_ld + y_off + c, vy);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) va[k] = (b ? va[k] + vb[k] : va[k]) + (accumulate ? vy[k] : 0.0f);
-      Vec8<T>::store(y + pix * y_ld + y_off + c, va);
-    }
-  } else {
-    const long base = blockIdx.x * (256l * U) + threadIdx.x;
-    float va[U][8], vb[U][8], vy[U][8];
-    long yo[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long it = base + u * 256l;
-      yo[u] = -1;
-      if (it < items) {
-        const long pix = it / cg;
-        const int c = (int)(it - pix * cg) * 8;
-        yo[u] = pix * y_ld + y_off + c;
-        Vec8<T>::load(a + pix * a_ld + a_off + c, va[u]);
-        if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb[u]);
-        if (accumulate) Vec8<T>::load(y + yo[u], vy[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (yo[u] < 0) continue;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) va[u][k] = (b ? va[u][k] + vb[u][k] : va[u][k]) + (accumulate ? vy[u][k] : 0.0f);
-      Vec8<T>::store(y + yo[u], va[u]);
-    }
+    for (int k = 0; k < 8; ++k) va[k] = (b ? va[k] + vb[k] : va[k]) + (accumulate ? vy[k] : 0.0f);
+    Vec8<T>::store(y + pix * y_ld + y_off + c, va);
   }
 }
 
-// Backward of y = a + b: g -> ga (+)= g and gb (+)= g in one pass (g read once); U as above
-template <typename T, int U>
+// Backward of y = a + b: g -> ga (+)= g and gb (+)= g in one pass (g read once)
+template <typename T>
 __global__ __launch_bounds__(256) void add_grad2_kernel(long items, int cg, const T* g, int g_ld, int g_off, T* y1,
                                                         int ld1, int off1, int acc1, T* y2, int ld2, int off2,
                                                         int acc2) {
-  if constexpr (U == 0) {
-    for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
-      const long pix = it / cg;
-      const int c = (int)(it - pix * cg) * 8;
-      float vg[8], v1[8], v2[8];
-      Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
-      if (acc1) Vec8<T>::load(y1 + pix * ld1 + off1 + c, v1);
-      if (acc2) Vec8<T>::load(y2 + pix * ld2 + off2 + c, v2);
+  for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
+    const long pix = it / cg;
+    const int c = (int)(it - pix * cg) * 8;
+    float vg[8], v1[8], v2[8];
+    Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
+    if (acc1) Vec8<T>::load(y1 + pix * ld1 + off1 + c, v1);
+    if (acc2) Vec8<T>::load(y2 + pix * ld2 + off2 + c, v2);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v1[k] = acc1 ? v1[k] + vg[k] : vg[k];
-        v2[k] = acc2 ? v2[k] + vg[k] : vg[k];
-      }
-      Vec8<T>::store(y1 + pix * ld1 + off1 + c, v1);
-      Vec8<T>::store(y2 + pix * ld2 + off2 + c, v2);
+    for (int k = 0; k < 8; ++k) {
+      v1[k] = acc1 ? v1[k] + vg[k] : vg[k];
+      v2[k] = acc2 ? v2[k] + vg[k] : vg[k];
     }
-  } else {
-    const long base = blockIdx.x * (256l * U) + threadIdx.x;
-    float vg[U][8], v1[U][8], v2[U][8];
-    long o1[U], o2[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long it = base + u * 256l;
-      o1[u] = -1;
-      o2[u] = 0;
-      if (it < items) {
-        const long pix = it / cg;
-        const int c = (int)(it - pix * cg) * 8;
-        o1[u] = pix * ld1 + off1 + c;
-        o2[u] = pix * ld2 + off2 + c;
-        Vec8<T>::load(g + pix * g_ld + g_off + c, vg[u]);
-        if (acc1) Vec8<T>::load(y1 + o1[u], v1[u]);
-        if (acc2) Vec8<T>::load(y2 + o2[u], v2[u]);
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (o1[u] < 0) continue;
-#pragma unroll
-      for (int k = 0; k < 8; ++k) {
-        v1[u][k] = acc1 ? v1[u][k] + vg[u][k] : vg[u][k];
-        v2[u][k] = acc2 ? v2[u][k] + vg[u][k] : vg[u][k];
-      }
-      Vec8<T>::store(y1 + o1[u], v1[u]);
-      Vec8<T>::store(y2 + o2[u], v2[u]);
-    }
+    Vec8<T>::store(y1 + pix * ld1 + off1 + c, v1);
+    Vec8<T>::store(y2 + pix * ld2 + off2 + c, v2);
   }
 }
+static unsigned add_grid(long items) { return (unsigned)std::min<long>((items + 255) / 256, 16384); }
 
 }  // namespace yms
 
@@ -1324,13 +948,11 @@ int yms_dwconv_stats_rows(const yms_dw_shape* s) {
   return dw_fwd_tiles(s, tx, ty);
 }
 
-static yms_status dw_fwd_impl(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
-                              int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
-                              int stats_ld, const float* isc, const float* ish, int iact, void* stream) {
+yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
+                          int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
+                          int stats_ld, void* stream) {
   if (!dw_shape_ok(s) || !x || !w || !y || !dw_view_ok(x_ld, x_off, s->c) || !dw_view_ok(y_ld, y_off, s->c))
     return YMS_ERR_INVALID;
-  const bool bnin = isc != nullptr;
-  if (bnin && (!ish || !stats || s->dtype == YMS_F32)) return YMS_ERR_INVALID;
   if (stats && stats_ld < s->c) return YMS_ERR_INVALID;
   if (!dw_image_fits(s, x_ld) || !dw_image_fits(s, y_ld)) return YMS_ERR_UNSUPPORTED;
   if (stats && (long)yms_dwconv_stats_rows(s) * 2 * stats_ld * 4 >= (long)NT_OOB) return YMS_ERR_UNSUPPORTED;
@@ -1340,20 +962,9 @@ static yms_status dw_fwd_impl(const yms_dw_shape* s, const void* x, int x_ld, in
   p.scale = scale; p.shift = shift; p.act = act; p.stats = stats; p.stats_ld = stats_ld;
   if (stats) p.stats_cnt = stats + (long)yms_dwconv_stats_rows(s) * 2 * stats_ld;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  p.isc = isc; p.ish = ish; p.iact = iact;
   const dim3 grid = dw_strip_grid(s, p);
   hipStream_t st = (hipStream_t)stream;
   const int TX = dw_fwd_tx(s);
-  if (bnin) {
-    if (dw_fwd_g(s) == 8) {
-      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_STATS_BNIN, TXX, 8>), grid,
-                                                             dim3(512), 0, st, p)));
-      return launch_status();
-    }
-    YMS_DW_T16(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_STATS_BNIN, TXX>),
-                                                                         grid, dim3(256), 0, st, p))));
-    return launch_status();
-  }
   if (dw_fwd_g(s) == 8) {
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
       if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_STATS, TXX, 8>), grid, dim3(512), 0, st, p);
@@ -1366,21 +977,6 @@ static yms_status dw_fwd_impl(const yms_dw_shape* s, const void* x, int x_ld, in
     else hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_AFFINE, TXX>), grid, dim3(256), 0, st, p);
   })));
   return launch_status();
-}
-
-yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const float* w, void* y,
-                          int y_ld, int y_off, const float* scale, const float* shift, int act, float* stats,
-                          int stats_ld, void* stream) {
-  return dw_fwd_impl(s, x, x_ld, x_off, w, y, y_ld, y_off, scale, shift, act, stats, stats_ld, nullptr, nullptr, 0,
-                     stream);
-}
-
-yms_status yms_dwconv_fwd_bnin(const yms_dw_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
-                               const float* in_shift, int in_act, const float* w, void* y, int y_ld, int y_off,
-                               float* stats, int stats_ld, void* stream) {
-  if (!in_scale) return YMS_ERR_INVALID;
-  return dw_fwd_impl(s, z, z_ld, z_off, w, y, y_ld, y_off, nullptr, nullptr, 0, stats, stats_ld, in_scale, in_shift,
-                     in_act, stream);
 }
 
 yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w, void* dx,
@@ -1405,112 +1001,37 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
   return launch_status();
 }
 
-int yms_dwconv_dgrad_rows(const yms_dw_shape* s) {
-  if (!dw_shape_ok(s)) return 0;
-  DwParams p{};
-  return (int)dw_strip_grid(s, p).x;
-}
-
-yms_status yms_dwconv_dgrad_bnred(const yms_dw_shape* s, const void* dz, int dz_ld, int dz_off, const float* w,
-                                  void* dx, int dx_ld, int dx_off, const void* rz, int rz_ld, int rz_off,
-                                  const float* rscale, const float* rshift, const float* rmean_invstd, int ract,
-                                  float* rws, void* stream) {
-  if (!dw_shape_ok(s) || !dz || !w || !dx || !rz || !rscale || !rshift || !rmean_invstd || !rws ||
-      !dw_view_ok(dz_ld, dz_off, s->c) || !dw_view_ok(dx_ld, dx_off, s->c) || !dw_view_ok(rz_ld, rz_off, s->c))
-    return YMS_ERR_INVALID;
-  if (!dw_image_fits(s, dz_ld) || !dw_image_fits(s, dx_ld)) return YMS_ERR_UNSUPPORTED;
-  DwParams p{};
-  p.src = (const char*)dz; p.src_ld = dz_ld; p.src_off = dz_off; p.w = w;
-  p.dst = (char*)dx; p.dst_ld = dx_ld; p.dst_off = dx_off; p.accumulate = 0;
-  p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  p.rz = (const char*)rz; p.rz_ld = rz_ld; p.rz_off = rz_off;
-  p.rsc = rscale; p.rsh = rshift; p.rmi = rmean_invstd; p.ract = ract; p.rws = rws;
-  const dim3 grid = dw_strip_grid(s, p);
-  hipStream_t st = (hipStream_t)stream;
-  const int TX = dw_fwd_tx(s);
-  if (dw_fwd_g(s) == 8) {
-    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_DGRAD_RED, TXX, 8>), grid,
-                                                           dim3(512), 0, st, p)));
-    return launch_status();
-  }
-  YMS_DW_T(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_DGRAD_RED, TXX>),
-                                                                     grid, dim3(256), 0, st, p))));
-  return launch_status();
-}
-
 size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s) {
   if (!dw_shape_ok(s)) return 0;
+  const size_t row = (size_t)s->k * s->k * s->c * sizeof(float);
   if (dw_wg3(s)) {
     DwParams p{};
-    return (size_t)dw_wg3_grid(s, p).x * s->k * s->k * s->c * sizeof(float);
+    return (size_t)dw_wg3_grid(s, p).x * row;
   }
-  size_t tile = (size_t)dw_wgrad_blocks(s) * s->k * s->k * s->c * sizeof(float);
-  if (dw_wg2(s)) tile = std::max(tile, (size_t)dw_wg2_blocks(s) * s->k * s->k * s->c * sizeof(float));
-  if (dw_wgk(s)) {
-    // the input-affine (BNIN) weight gradient keeps the tile kernel: size for both
-    DwParams p{};
-    return std::max(tile, (size_t)dw_wgk_grid(s, p).x * s->k * s->k * s->c * sizeof(float));
-  }
-  return tile;
+  return (size_t)(dw_wg2(s) ? dw_wg2_blocks(s) : dw_wgrad_blocks(s)) * row;
 }
 
-static yms_status dw_wgrad_impl(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
-                                int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, const float* isc,
-                                const float* ish, int iact, void* stream) {
+yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
+                            int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream) {
   if (!dw_shape_ok(s) || !x || !dz || !ws || !dw || !dw_view_ok(x_ld, x_off, s->c) || !dw_view_ok(dz_ld, dz_off, s->c))
     return YMS_ERR_INVALID;
   if (ws_bytes < yms_dwconv_wgrad_ws_bytes(s)) return YMS_ERR_INVALID;
-  const bool bnin = isc != nullptr;
-  if (bnin && (!ish || s->dtype == YMS_F32)) return YMS_ERR_INVALID;
   DwParams p{};
   p.src = (const char*)x; p.src_ld = x_ld; p.src_off = x_off;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  p.isc = isc; p.ish = ish; p.iact = iact;
+  hipStream_t st = (hipStream_t)stream;
+  const int KK2 = s->k * s->k;
+  int blocks;
   if (dw_wg3(s)) {
     if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
     const dim3 grid = dw_wg3_grid(s, p);
-    hipStream_t st = (hipStream_t)stream;
     const int TX = dw_fwd_tx(s);
-    if (bnin) {
-      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 4, true>), grid,
-                                                             dim3(256), 0, st, p, (const char*)dz, dz_ld, dz_off, ws)));
-    } else if (dw_wg3_g(s) == 8) {
-      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 8>), grid, dim3(512), 0,
-                                                             st, p, (const char*)dz, dz_ld, dz_off, ws)));
-    } else {
-      YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 4>), grid, dim3(256), 0,
-                                                             st, p, (const char*)dz, dz_ld, dz_off, ws)));
-    }
-    yms_status e = launch_status();
-    if (e != YMS_OK) return e;
-    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * 9 + 63) / 64)), dim3(1024), 0, st, ws,
-                       (int)grid.x, s->c, 9, dw, accumulate);
-    return launch_status();
-  }
-  if (dw_wgk(s) && !bnin) {
-    if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
-    const dim3 grid = dw_wgk_grid(s, p);
-    hipStream_t st = (hipStream_t)stream;
-    const int TX = dw_fwd_tx(s);
-    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
-      if (s->k == 5) hipLaunchKernelGGL((dwconv_wgradk_kernel<TT, 5, TXX>), grid, dim3(5 * 64), 0, st, p,
-                                        (const char*)dz, dz_ld, dz_off, ws);
-      else if (s->k == 7) hipLaunchKernelGGL((dwconv_wgradk_kernel<TT, 7, TXX>), grid, dim3(7 * 64), 0, st, p,
-                                             (const char*)dz, dz_ld, dz_off, ws);
-      else hipLaunchKernelGGL((dwconv_wgradk_kernel<TT, 9, TXX>), grid, dim3(9 * 64), 0, st, p, (const char*)dz,
-                              dz_ld, dz_off, ws);
-    }));
-    yms_status e = launch_status();
-    if (e != YMS_OK) return e;
-    const int KK2 = s->k * s->k;
-    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
-                       (int)grid.x, s->c, KK2, dw, accumulate);
-    return launch_status();
-  }
-  if (dw_wg2(s) && !bnin) {
-    const int blocks = dw_wg2_blocks(s);
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 4>), grid, dim3(256), 0, st,
+                                                           p, (const char*)dz, dz_ld, dz_off, ws)));
+    blocks = (int)grid.x;
+  } else if (dw_wg2(s)) {
+    blocks = dw_wg2_blocks(s);
     const dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
-    hipStream_t st = (hipStream_t)stream;
     const int TX = dw_fwd_tx(s);
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
       if (s->k == 5) hipLaunchKernelGGL((dwconv_wgrad2_kernel<TT, 5, TXX>), grid, dim3(DW_WG_NT), 0, st, p,
@@ -1520,53 +1041,18 @@ static yms_status dw_wgrad_impl(const yms_dw_shape* s, const void* x, int x_ld, 
       else hipLaunchKernelGGL((dwconv_wgrad2_kernel<TT, 9, TXX>), grid, dim3(DW_WG_NT), 0, st, p, (const char*)dz,
                               dz_ld, dz_off, ws);
     }));
-    yms_status e = launch_status();
-    if (e != YMS_OK) return e;
-    const int KK2 = s->k * s->k;
-    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
-                       blocks, s->c, KK2, dw, accumulate);
-    return launch_status();
-  }
-  dw_tiles(s, p.tiles_x, p.tiles_y);
-  const int blocks = dw_wgrad_blocks(s);
-  dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
-  hipStream_t st = (hipStream_t)stream;
-  if (bnin) {
-    YMS_DW_T16(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK, true>), grid, dim3(DW_WG_NT), 0,
-                                                          st, p, (const char*)dz, dz_ld, dz_off, ws)));
   } else {
+    dw_tiles(s, p.tiles_x, p.tiles_y);
+    blocks = dw_wgrad_blocks(s);
+    const dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
     YMS_DW_T(s->dtype, YMS_DW_K(s->k, hipLaunchKernelGGL((dwconv_wgrad_kernel<TT, KK>), grid, dim3(DW_WG_NT), 0, st, p,
                                                         (const char*)dz, dz_ld, dz_off, ws)));
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
-  const int KK2 = s->k * s->k;
   hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
                      blocks, s->c, KK2, dw, accumulate);
   return launch_status();
-}
-
-yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int x_off, const void* dz, int dz_ld,
-                            int dz_off, float* ws, size_t ws_bytes, float* dw, int accumulate, void* stream) {
-  return dw_wgrad_impl(s, x, x_ld, x_off, dz, dz_ld, dz_off, ws, ws_bytes, dw, accumulate, nullptr, nullptr, 0, stream);
-}
-
-yms_status yms_dwconv_wgrad_bnin(const yms_dw_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
-                                 const float* in_shift, int in_act, const void* dz, int dz_ld, int dz_off, float* ws,
-                                 size_t ws_bytes, float* dw, int accumulate, void* stream) {
-  if (!in_scale) return YMS_ERR_INVALID;
-  return dw_wgrad_impl(s, z, z_ld, z_off, dz, dz_ld, dz_off, ws, ws_bytes, dw, accumulate, in_scale, in_shift, in_act,
-                       stream);
-}
-
-// 16-B items per thread of the branch-sum kernels (YMS_ADD_ITERS: 0 = grid-stride loop over at most
-// 16384 blocks, 1, 2, 4; read per call)
-static int add_iters() {
-  const char* e = getenv("YMS_ADD_ITERS");
-  return e ? std::max(0, atoi(e)) : 0;
-}
-static unsigned add_grid(long items, int u) {
-  return u == 0 ? (unsigned)std::min<long>((items + 255) / 256, 16384) : (unsigned)((items + 256l * u - 1) / (256l * u));
 }
 
 yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, int a_off, const void* b, int b_ld,
@@ -1575,16 +1061,9 @@ yms_status yms_add_views(int dtype, long npix, int c, const void* a, int a_ld, i
     return YMS_ERR_INVALID;
   if (b && !dw_view_ok(b_ld, b_off, c)) return YMS_ERR_INVALID;
   const long items = npix * (c / 8);
-  const int u = add_iters();
-#define YMS_ADDV(UU)                                                                                             \
-  YMS_DW_T(dtype, hipLaunchKernelGGL((add_views_kernel<TT, UU>), dim3(add_grid(items, UU)), dim3(256), 0,          \
-                                     (hipStream_t)stream, items, c / 8, (const TT*)a, a_ld, a_off, (const TT*)b, b_ld, \
-                                     b_off, (TT*)y, y_ld, y_off, accumulate))
-  if (u == 0) YMS_ADDV(0);
-  else if (u == 1) YMS_ADDV(1);
-  else if (u == 2) YMS_ADDV(2);
-  else YMS_ADDV(4);
-#undef YMS_ADDV
+  YMS_DW_T(dtype, hipLaunchKernelGGL((add_views_kernel<TT>), dim3(add_grid(items)), dim3(256), 0, (hipStream_t)stream,
+                                     items, c / 8, (const TT*)a, a_ld, a_off, (const TT*)b, b_ld, b_off, (TT*)y, y_ld,
+                                     y_off, accumulate));
   return launch_status();
 }
 
@@ -1594,16 +1073,9 @@ yms_status yms_add_grad2(int dtype, long npix, int c, const void* g, int g_ld, i
       !dw_view_ok(ld2, off2, c))
     return YMS_ERR_INVALID;
   const long items = npix * (c / 8);
-  const int u = add_iters();
-#define YMS_ADDG(UU)                                                                                            \
-  YMS_DW_T(dtype, hipLaunchKernelGGL((add_grad2_kernel<TT, UU>), dim3(add_grid(items, UU)), dim3(256), 0,         \
-                                     (hipStream_t)stream, items, c / 8, (const TT*)g, g_ld, g_off, (TT*)y1, ld1, off1, \
-                                     acc1, (TT*)y2, ld2, off2, acc2))
-  if (u == 0) YMS_ADDG(0);
-  else if (u == 1) YMS_ADDG(1);
-  else if (u == 2) YMS_ADDG(2);
-  else YMS_ADDG(4);
-#undef YMS_ADDG
+  YMS_DW_T(dtype, hipLaunchKernelGGL((add_grad2_kernel<TT>), dim3(add_grid(items)), dim3(256), 0, (hipStream_t)stream,
+                                     items, c / 8, (const TT*)g, g_ld, g_off, (TT*)y1, ld1, off1, acc1, (TT*)y2, ld2,
+                                     off2, acc2));
   return launch_status();
 }
 

@@ -639,8 +639,10 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-__global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, int grid_min_kept,
-                                                              int win_max, NmsWs ws) {
+// grid lookups from this many kept boxes on (below, the 16-way split of the whole kept list is as fast)
+constexpr int NMS_GRID_MIN_KEPT = 128;
+
+__global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
   extern __shared__ float4 s_kept[];                              // [NMS_KEPT_LDS]
   uint16_t* s_cell = reinterpret_cast<uint16_t*>(s_kept + NMS_KEPT_LDS);   // [NMS_CELLS][CAP]
   int* s_ccnt = reinterpret_cast<int*>(s_cell + NMS_CELLS * NMS_CELL_CAP);  // [NMS_CELLS]
@@ -653,7 +655,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
     const int n = ws.cls_cnt[(long)b * nc + c];
-    if (n <= win_max || ws.route[(long)b * nc + c] != 3) continue;   // block-uniform: window / wgrid / graph kernels'
+    if (ws.route[(long)b * nc + c] != 3) continue;   // block-uniform: wgrid / graph kernels'
     const int off = ws.cls_off[(long)b * nc + c];
     float4* boxes = ws.gboxes + (long)b * A + off;
     int* idx = ws.scratch + (long)b * A + off;
@@ -741,7 +743,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
         ncell = nx * (nms_cell(cb.w, oy, invy, gy) - y0 + 1);
       }
       bool sup = false;
-      if (has && use_grid && nk >= grid_min_kept) {
+      if (has && use_grid && nk >= NMS_GRID_MIN_KEPT) {
         if (cvalid) {
           // slot ncell = the wide-box list; slots [0, ncell) the covered cells, split over waves
           for (int q = wave; q <= ncell && !sup; q += 16) {
@@ -839,132 +841,6 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
              pacc[0], pacc[1], pacc[2], pacc[3], pacc[4], pacc[5]);
 #endif
 #undef PMARK
-    if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
-    __syncthreads();
-  }
-}
-
-// Greedy suppression of a sorted big segment of at most NMS_WIN_MAX boxes, by WINDOWS of kept-box
-// candidates (opt-in, YMS_NMS_WINDOW=1; nms_big_greedy_kernel is the default, see the dispatch).  The
-// block stages the segment's boxes in LDS with an alive bit per box and repeats:
-//   1. wave 0 takes the next (up to) 64 alive candidates in score order (the window),
-//   2. resolves them serially among themselves (a candidate survives unless a kept window member
-//      before it overlaps it: greedy order) and appends the survivors to the kept list,
-//   3. all 16 waves test every alive candidate after the window against this window's kept boxes
-//      only, clearing the alive bits of those suppressed.
-// Every candidate reaching a window has already been tested against every box kept before it
-// (step 3 of each earlier round), so each window member's fate equals sequential greedy NMS: the
-// keep list is the same, in the same order.  Work is (candidates x kept boxes) spread over 1024
-// threads with no per-64-candidate barrier chain; the kept-list greedy above walks the segment in
-// 64-candidate steps, each a test phase, a serial resolve and a grid insert behind barriers.
-constexpr int NMS_WIN_MAX = 8192;
-constexpr size_t NMS_WIN_LDS = (size_t)NMS_WIN_MAX * 16;
-
-__global__ __launch_bounds__(1024) void nms_window_kernel(int A, int nc, float thr_f, int full, NmsWs ws) {
-  extern __shared__ float4 s_box[];                   // [NMS_WIN_MAX] sorted boxes of the segment
-  __shared__ uint32_t s_alive[NMS_WIN_MAX / 32];
-  __shared__ float4 s_kw[64];                         // boxes kept in this round's window
-  __shared__ int s_win[64];
-  __shared__ int s_m, s_kn, s_nk, s_cw, s_wend;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nbig = ws.big[0];
-  for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
-    const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
-    const int n = ws.cls_cnt[(long)b * nc + c];
-    if (n > NMS_WIN_MAX || ws.route[(long)b * nc + c] != 3) continue;   // block-uniform: big greedy / wgrid / graph
-    const int off = ws.cls_off[(long)b * nc + c];
-    float4* boxes = ws.gboxes + (long)b * A + off;
-    int* idx = ws.scratch + (long)b * A + off;
-    const int nw = (n + 31) >> 5;
-    for (int i = tid; i < n; i += 1024) s_box[i] = boxes[i];
-    for (int w = tid; w < nw; w += 1024)
-      s_alive[w] = (w == nw - 1 && (n & 31)) ? ((1u << (n & 31)) - 1u) : 0xffffffffu;
-    if (tid == 0) { s_nk = 0; s_cw = 0; }
-    __syncthreads();
-    for (;;) {
-      // ---- 1. window: the next (up to) 64 alive candidates, in order ----
-      if (wave == 0) {
-        int m = 0, cw = s_cw;
-        while (m < 64 && cw < nw) {
-          const uint32_t wd = cw + lane < nw ? s_alive[cw + lane] : 0u;
-          const int pc = __popc(wd);
-          int incl = pc;
-#pragma unroll
-          for (int d = 1; d < 64; d <<= 1) {
-            const int t = __shfl_up(incl, d);
-            if (lane >= d) incl += t;
-          }
-          const int excl = incl - pc, tot = __shfl(incl, 63);
-          uint32_t bits = wd;
-          for (int r = m + excl; bits && r < 64; ++r) {
-            s_win[r] = ((cw + lane) << 5) + __ffs(bits) - 1;
-            bits &= bits - 1u;
-          }
-          if (m + tot >= 64) {          // the window ends inside the word holding rank 63
-            const unsigned long long h = __ballot(m + excl <= 63 && 63 < m + incl);
-            cw += __ffsll((long long)h) - 1;
-            m = 64;
-          } else {
-            m += tot;
-            cw += 64;
-          }
-        }
-        if (lane == 0) { s_m = m; s_cw = min(cw, nw); }
-      }
-      __syncthreads();
-      const int m = s_m;
-      if (m == 0) break;
-      // ---- 2. resolve the window (wave 0) ----
-      if (wave == 0) {
-        const bool has = lane < m;
-        const int j = has ? s_win[lane] : 0;
-        const float4 cb = has ? s_box[j] : make_float4(0.f, 0.f, 0.f, 0.f);
-        const int cid = has ? idx[j] : 0;
-        bool alive = has;
-        unsigned long long am = __ballot(alive), done = 0;
-        for (;;) {
-          const unsigned long long rem = am & ~done;
-          if (!rem) break;
-          const int i = __builtin_ctzll(rem);     // wave-uniform
-          done |= 1ull << i;
-          float4 bi;
-          bi.x = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.x), i));
-          bi.y = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.y), i));
-          bi.z = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.z), i));
-          bi.w = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, cb.w), i));
-          if (alive && lane > i && iou_gt_f(bi, cb, thr_f, full)) alive = false;
-          am = __ballot(alive);
-        }
-        const int nk = s_nk, kn = __popcll(am);
-        const int rank = __popcll(am & ((1ull << lane) - 1ull));
-        if (alive) {          // nk + rank <= j: only consumed slots are overwritten
-          s_kw[rank] = cb;
-          boxes[nk + rank] = cb;
-          idx[nk + rank] = cid;
-        }
-        const int wend = __shfl(j, m - 1);
-        if (lane == 0) { s_kn = kn; s_nk = nk + kn; s_wend = wend; }
-      }
-      __syncthreads();
-      // ---- 3. every alive candidate after the window vs this window's kept boxes ----
-      const int kn = s_kn, wend = s_wend;
-      for (int base = wave * 64; base < n; base += 1024) {
-        const int j = base + lane;
-        const uint32_t wd = s_alive[(base >> 5) + (lane >> 5)];
-        bool a = j < n && j > wend && ((wd >> (j & 31)) & 1u);
-        if (a && kn > 0) {
-          const float4 cb = s_box[j];
-          for (int k = 0; k < kn; ++k)
-            if (iou_gt_f(s_kw[k], cb, thr_f, full)) { a = false; break; }
-        }
-        const unsigned long long bl = __ballot(a);
-        if (lane == 0) {
-          if ((base >> 5) < nw) s_alive[base >> 5] = (uint32_t)bl;
-          if ((base >> 5) + 1 < nw) s_alive[(base >> 5) + 1] = (uint32_t)(bl >> 32);
-        }
-      }
-      __syncthreads();
-    }
     if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
     __syncthreads();
   }
@@ -2136,8 +2012,6 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
                             NMS_CHUNK * 8) != hipSuccess ||
         hipFuncSetAttribute((const void*)nms_big_greedy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)NMS_GREEDY_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void*)nms_window_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)NMS_WIN_LDS) != hipSuccess ||
         hipFuncSetAttribute((const void*)nms_wgrid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)NMS_WG_LDS) != hipSuccess)
       return YMS_ERR_LAUNCH;
@@ -2165,30 +2039,16 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
       hipLaunchKernelGGL(nms_graph_resolve_kernel, dim3(gsegs), dim3(1024), (size_t)NMS_GR_MAXN * 12, st, A, nc,
                          thr_f, tr, w);
     }
-    // 3. the rest (route 3): sorted, then the kept-list greedy (or the opt-in window kernel)
+    // 3. the rest (route 3): sorted, then the kept-list greedy
     if (A > NMS_CHUNK)
       hipLaunchKernelGGL(nms_chunk_sort_kernel, dim3(256), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc, w);
     hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc,
                        boxes_xyxy, w);
-    // grid lookups from this many kept boxes on (below, the 16-way split of the whole kept list
-    // is as fast); YMS_NMS_GRID_MIN_KEPT overrides it for A/B measurements
-    static const int grid_min = [] {
-      const char* e = getenv("YMS_NMS_GRID_MIN_KEPT");
-      return e ? atoi(e) : 128;
-    }();
-    // YMS_NMS_WINDOW=1: segments of at most NMS_WIN_MAX boxes on the window kernel (opt-in, read
-    // per call).  Measured (profiles/r04c_nms_kernels.txt): 267 vs 343 us on the bench's level
-    // segments (~115 kept of 6400), but 4.0 ms on uniform small boxes where most candidates are kept
-    // (its test phase is candidates x kept boxes on one CU; the grid greedy prunes spatially).
-    const char* wenv = getenv("YMS_NMS_WINDOW");
-    const int win_max = (wenv && atoi(wenv) == 1) ? NMS_WIN_MAX : 0;
     // the window-grid greedy over global memory for sorted finite segments of NMS_WG_MAX..NMS_WGG_MAX
     if (!full && wg_on && A > NMS_WG_MAX)
       hipLaunchKernelGGL(nms_wgrid_glb_kernel, dim3(segs), dim3(1024), 0, st, A, nc, thr_f, tr, w);
-    if (win_max > 0)
-      hipLaunchKernelGGL(nms_window_kernel, dim3(segs), dim3(1024), NMS_WIN_LDS, st, A, nc, thr_f, full, w);
     hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
-                       thr_f, full, grid_min, win_max, w);
+                       thr_f, full, w);
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;

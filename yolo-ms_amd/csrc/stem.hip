@@ -493,8 +493,6 @@ static int stem_tiles(const yms_conv_shape* s, int& tx, int& ty) {
 
 // strips of tps tiles: about `target` blocks, so each block walks several tiles
 static unsigned stem_strips(const yms_conv_shape* s, StemParams& p, long target) {
-  static const long env = getenv("YMS_STEM_BLOCKS") ? std::max(1, atoi(getenv("YMS_STEM_BLOCKS"))) : 0;
-  if (env) target = env;
   const long cols = (long)s->n * p.tiles_x;
   const int want = (int)std::max(1l, std::min<long>(p.tiles_y, (target + cols - 1) / cols));
   p.tps = (p.tiles_y + want - 1) / want;

@@ -245,21 +245,13 @@ bool wgrad_halo_plan(const yms_conv_shape* s, WHPlan* w) {
   q.S = s->stride;
   q.mb = s->cout <= 32 ? 1 : 2;
   q.nb = 1;
-  // "small" (default): <= 64 KB of LDS per block, so the side-stream weight gradients fit on a CU
-  // beside the main stream's conv blocks (a 120-150 KB block waits for a whole CU to drain: in the
-  // training step that cost more than the nine-fold input re-read it removes); "big"
-  // (YMS_WG_HALO_BIG=1): 256 / 128-pixel patches in 112-150 KB, faster in isolation
-  static const int big = env_int_wh("YMS_WG_HALO_BIG", 0);
-  q.big = big;
-  if (big) {
-    q.wk = q.mb == 1 ? 4 : 2;
-    q.kp = q.S == 1 ? 256 : 128;
-    q.hb = q.S == 1 ? 384 : 640;
-  } else {
-    q.wk = q.mb == 1 ? 2 : 1;
-    q.kp = q.S == 1 ? 128 : 64;
-    q.hb = q.S == 1 ? 256 : 384;
-  }
+  // <= 64 KB of LDS per block, so the side-stream weight gradients fit on a CU beside the main
+  // stream's conv blocks (round 3, measured and dropped: 256 / 128-pixel patches in 112-150 KB,
+  // faster in isolation, but such a block waits for a whole CU to drain: in the training step that
+  // cost more than the nine-fold input re-read it removes)
+  q.wk = q.mb == 1 ? 2 : 1;
+  q.kp = q.S == 1 ? 128 : 64;
+  q.hb = q.S == 1 ? 256 : 384;
   q.TW = std::min(pick_tw(s->wo), q.kp);
   q.R = std::max(1, std::min(s->ho, q.kp / q.TW));
   for (;;) {
@@ -282,8 +274,7 @@ bool wgrad_halo_plan(const yms_conv_shape* s, WHPlan* w) {
   const int tiles = q.tiles_co * q.tiles_ci;
   // about two blocks per CU in all; each split writes (and the reduce re-reads) one fp32 slab, so
   // cap the slab round trip at the layer's own x + dz bytes (keeping >= 256 blocks)
-  static const int bpc = std::max(1, env_int_wh("YMS_WG_HALO_BPC", 2));
-  int splits = std::max(1, std::min(q.npatch, cdiv((long)bpc * conv_cu_count(), tiles)));
+  int splits = std::max(1, std::min(q.npatch, cdiv(2l * conv_cu_count(), tiles)));
   const double data = (double)s->n * s->ho * s->wo * rup(s->cout, 8) * 2.0 + (double)s->n * s->h * s->w * cin8 * 2.0;
   const double slab_rt = 2.0 * 4.0 * (double)q.slab_rows * q.slab_ld * q.wk;
   const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;   // see conv_igemm.hip
@@ -304,21 +295,11 @@ static void launch_wh(const WHParams& p, int blocks, hipStream_t st) {
 template <typename T>
 static void dispatch_wh(const WHPlan& w, const WHParams& p, int blocks, hipStream_t st) {
   if (w.S == 1) {
-    if (w.big) {
-      if (w.mb == 1) launch_wh<T, 1, 1, 1, 4, 256, 384, 3>(p, blocks, st);
-      else launch_wh<T, 1, 2, 1, 2, 256, 384, 2>(p, blocks, st);
-    } else {
-      if (w.mb == 1) launch_wh<T, 1, 1, 1, 2, 128, 256, 2>(p, blocks, st);
-      else launch_wh<T, 1, 2, 1, 1, 128, 256, 2>(p, blocks, st);
-    }
+    if (w.mb == 1) launch_wh<T, 1, 1, 1, 2, 128, 256, 2>(p, blocks, st);
+    else launch_wh<T, 1, 2, 1, 1, 128, 256, 2>(p, blocks, st);
   } else {
-    if (w.big) {
-      if (w.mb == 1) launch_wh<T, 2, 1, 1, 4, 128, 640, 2>(p, blocks, st);
-      else launch_wh<T, 2, 2, 1, 2, 128, 640, 2>(p, blocks, st);
-    } else {
-      if (w.mb == 1) launch_wh<T, 2, 1, 1, 2, 64, 384, 2>(p, blocks, st);
-      else launch_wh<T, 2, 2, 1, 1, 64, 384, 2>(p, blocks, st);
-    }
+    if (w.mb == 1) launch_wh<T, 2, 1, 1, 2, 64, 384, 2>(p, blocks, st);
+    else launch_wh<T, 2, 2, 1, 1, 64, 384, 2>(p, blocks, st);
   }
 }
 

@@ -6,7 +6,7 @@
 namespace yms {
 
 struct WHPlan {
-  int S, mb, nb, wk, kp, hb, big;     // kernel variant: stride, co / ci 32-blocks, k-step wave groups,
+  int S, mb, nb, wk, kp, hb;          // kernel variant: stride, co / ci 32-blocks, k-step wave groups,
                                       // pixels and halo capacity
   int TW, R, HR, HC;                  // patch of R x TW output pixels, halo of HR x HC input pixels
   int ptx, pty, npatch, splits, pps;  // patches per row / column, total, splits over patches, per split

@@ -209,8 +209,8 @@ static int env_int_wr(const char* name, int dflt) {
   return v ? atoi(v) : dflt;
 }
 
-// variant (YMS_WG_RING_VAR, dev A/B): 0 = KP 64 / ST 2 / 2 blocks per CU, 1 = KP 32 / ST 4 / 2
-// (128 x 128 tiles only), 2 = KP 64 / ST 3 / 1, 3 = KP 32 / ST 2 / 4 (32 KB: 128 x 128 only)
+// 64-pixel k-tiles, 2 stages, 2 blocks per CU (round 4, measured and dropped: 32-pixel k-tiles with
+// 2 / 4 stages, 3 stages at 1 block per CU, and the 64 x 64 GEMMs on zero-filled 64 x 128 tiles)
 bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
   const int on = env_int_wr("YMS_WG_RING", 1);   // read per call: tests switch it at run time
   if (!on || s->dtype == YMS_F32 || (s->k != 1 && s->k != 3)) return false;
@@ -223,17 +223,9 @@ bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
   // register-staged kernel (its 32-row / 64-column tiles) unless YMS_WG_RING=2
   q.bm = s->cout <= 64 ? 64 : 128;
   q.bn = kf <= 64 ? 64 : 128;
-  // YMS_WG_RING_SMALL=1 (dev A/B): the 64 x 64 GEMMs (and <= 32 output channels) on a 64 x 128 ring
-  // tile, the unused columns zero-filled by the range check (no bytes fetched for them)
-  const int small = env_int_wr("YMS_WG_RING_SMALL", 0);   // per call: dev tools switch it
-  if (q.bm == 64 && q.bn == 64) {
-    if (!small) return false;
-    q.bn = 128;
-  }
-  if (on != 2 && !small && s->cout <= 32) return false;
-  const int var = env_int_wr("YMS_WG_RING_VAR", 0);
-  q.var = ((var == 1 || var == 3) && !(q.bm == 128 && q.bn == 128)) ? 0 : var;
-  q.kp = (q.var == 1 || q.var == 3) ? 32 : 64;
+  if (q.bm == 64 && q.bn == 64) return false;
+  if (on != 2 && s->cout <= 32) return false;
+  q.kp = 64;
   q.tiles_m = cdiv(s->cout, q.bm);
   q.tiles_n = cdiv(kf, q.bn);
   q.slab_rows = q.tiles_m * q.bm;
@@ -242,15 +234,13 @@ bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
   if (M >= (1l << 30)) return false;
   q.nkt = cdiv(M, q.kp);
   const int blocks = q.tiles_m * q.tiles_n;
-  // about `bpc` blocks per CU, at least 8 k-tiles per split; the slab round trip capped at the
-  // layer's own x + dz bytes (keeping >= 256 blocks), as for the register-staged kernel
-  static const int bpc = std::max(1, env_int_wr("YMS_WG_RING_BPC", 4));
-  int splits = std::max(1, std::min(cdiv(q.nkt, 8), cdiv((long)bpc * conv_cu_count(), blocks)));
+  // about 4 blocks per CU, at least 8 k-tiles per split; the slab round trip capped at a fraction
+  // of the layer's own x + dz bytes (keeping >= 256 blocks), as for the register-staged kernel
+  int splits = std::max(1, std::min(cdiv(q.nkt, 8), cdiv(4l * conv_cu_count(), blocks)));
   const double data = (double)M * (double)(rup(s->cout, 8) + q.cin8) * 2.0;
   const double slab_rt = 2.0 * 4.0 * (double)q.slab_rows * (double)q.slab_ld;
   const double ratio = getenv("YMS_WG_SLAB_RATIO") ? atof(getenv("YMS_WG_SLAB_RATIO")) : 0.05;   // see conv_igemm.hip
-  const int minb = std::max(1, env_int_wr("YMS_WG_RING_MINB", 256));   // dev A/B (read per call)
-  const int cap = std::max((int)(ratio * data / slab_rt), cdiv(minb, blocks));
+  const int cap = std::max((int)(ratio * data / slab_rt), cdiv(256, blocks));
   splits = std::max(1, std::min(splits, cap));
   q.kt_per_split = cdiv(q.nkt, splits);
   q.splits = cdiv(q.nkt, q.kt_per_split);
@@ -259,19 +249,8 @@ bool wgrad_ring_plan(const yms_conv_shape* s, WRPlan* w) {
 }
 
 template <typename T, int KS, int BM, int BN>
-static void launch_wr_t(const WRPlan& w, const WRParams& p, dim3 grid, hipStream_t st) {
-  if constexpr (BM == 128 && BN == 128) {
-    if (w.var == 1) {
-      hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, KS, BM, BN, 32, 4, 2>), grid, dim3(512), 0, st, p);
-      return;
-    }
-    if (w.var == 3) {
-      hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, KS, BM, BN, 32, 2, 4>), grid, dim3(512), 0, st, p);
-      return;
-    }
-  }
-  if (w.var == 2) hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, KS, BM, BN, 64, 3, 1>), grid, dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, KS, BM, BN, 64, 2, 2>), grid, dim3(512), 0, st, p);
+static void launch_wr_t(const WRPlan&, const WRParams& p, dim3 grid, hipStream_t st) {
+  hipLaunchKernelGGL((conv_wgrad_ring_kernel<T, KS, BM, BN, 64, 2, 2>), grid, dim3(512), 0, st, p);
 }
 
 template <typename T, int KS>

@@ -6,7 +6,7 @@
 namespace yms {
 
 struct WRPlan {
-  int bm, bn, kp, var;                       // tile rows (co) / columns (tap*cin8+ci), pixels per k-tile, variant
+  int bm, bn, kp;                            // tile rows (co) / columns (tap*cin8+ci), pixels per k-tile
   int cin8, cpt, kc;                         // input channels rounded to 8, 16-B chunks per tap, valid chunks
   int tiles_m, tiles_n, nkt, kt_per_split, splits, slab_rows, slab_ld;
 };

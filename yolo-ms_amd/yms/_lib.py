@@ -96,10 +96,6 @@ _SIGS = {
     "yms_dwconv_stats_rows": (_I, [_DP]),
     "yms_dwconv_fwd": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
     "yms_dwconv_dgrad": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
-    "yms_dwconv_dgrad_rows": (_I, [_DP]),
-    "yms_dwconv_fwd_bnin": (_I, [_DP, _P, _I, _I, _P, _P, _I, _P, _P, _I, _I, _P, _I, _P]),
-    "yms_dwconv_wgrad_bnin": (_I, [_DP, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
-    "yms_dwconv_dgrad_bnred": (_I, [_DP, _P, _I, _I, _P, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
     "yms_dwconv_wgrad_ws_bytes": (_SZ, [_DP]),
     "yms_dwconv_wgrad": (_I, [_DP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
     "yms_add_views": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _I, _I, _I, _P]),
@@ -150,8 +146,7 @@ def check(status, what):
 
 _prof = None
 _CONV = ("yms_conv_fwd", "yms_conv_fwd_pro", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd")
-_DW = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad", "yms_dwconv_dgrad_bnred", "yms_dwconv_fwd_bnin",
-       "yms_dwconv_wgrad_bnin")
+_DW = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
 # launches whose hipStream_t is the last argument (status-returning entry points ending in a void*)
 # (host-only entry points whose last pointer is a host buffer are listed out explicitly)
 _HOST_ONLY = {"yms_map_accumulate", "yms_pack_job_init"}
@@ -180,8 +175,7 @@ def _work(name, args):
     if name in _DW:
         d = args[0].contents
         vol = d.n * d.h * d.w * d.c
-        nio = 3 if name == "yms_dwconv_dgrad_bnred" else 2          # + the producer's z
-        return 2 * vol * d.k * d.k, nio * vol * _elt(d.dtype) + 4 * d.c * d.k * d.k
+        return 2 * vol * d.k * d.k, 2 * vol * _elt(d.dtype) + 4 * d.c * d.k * d.k
     if name in ("yms_bn_act_bwd_reduce", "yms_affine_act", "yms_bn_act_bwd_apply", "yms_add_views",
                 "yms_add_grad2"):
         vol = args[1] * args[2] * _elt(args[0])

@@ -29,10 +29,10 @@ import torch
 from . import _lib as L
 
 ALIGN = 256
-# BN backward finalize inside the reduce launch (last-arriving block, YMS_BN_FUSED=1) vs a separate
-# launch: the in-launch finalize puts one block's serial sum of the partial table on the critical path
-# (interleaved A/B, profiles/r02_ab_bn_fused_priority_graph.txt: 19.5-19.7 ms separate vs 20.4-21.3 ms fused)
-BN_FUSED_FINALIZE = os.environ.get("YMS_BN_FUSED", "0") == "1"
+# (the BN backward finalize inside the reduce launch -- last-arriving block -- was measured slower,
+# 19.5-19.7 ms separate vs 20.4-21.3 ms fused, profiles/r02_ab_bn_fused_priority_graph.txt: it puts one
+# block's serial sum of the partial table on the critical path; the fused launch serves the head's
+# bias gradients only, yms_bias_bwd)
 BN_MOMENTUM = 0.03   # components.py:73
 BN_EPS = 1e-3
 
@@ -240,8 +240,6 @@ class ConvOp:
         self.pb = b.param(mod.bn, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
-        self.red_rows = 0        # > 0: its BN-backward partial rows come from its consumer's dgrad
-        self.bnin_by = None      # depthwise consumer that forms act(BN(z)) itself (no affine pass)
         self.pro_by = None       # consumer conv that forms (and stores) this op's x = act(BN(z))
         self.pro = None          # producer whose act(BN(z)) this conv forms in its prologue
 
@@ -271,7 +269,6 @@ class ConvOp:
             self.bwd_rows = L.lib().yms_bn_bwd_rows(self.npix, c)
             plan.need_scratch("bwd", 4 * 2 * c * self.bwd_rows)
             plan.need_scratch("coef", 8 * c)
-            self.cnt = plan.counter()
             self.wg_ws = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
             plan.need_scratch("wgrad", self.wg_ws)
             if self.stem_input is not None:
@@ -331,7 +328,7 @@ class ConvOp:
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
-        if self.bnin_by is None and self.pro_by is None:
+        if self.pro_by is None:
             L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
                    base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
 
@@ -347,20 +344,10 @@ class ConvOp:
         ws = rt.gbase + rt.plan.gscratch["bwd"]
         coef = rt.gbase + rt.plan.gscratch["coef"]
         z = base + self.z
-        if self.red_rows:
-            # the partial rows were written by the consuming depthwise dgrad (DWConvOp.bnred)
-            L.call("yms_bn_act_bwd_finalize", c, ws, self.red_rows, self.npix,
-                   rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
-        elif BN_FUSED_FINALIZE:
-            # one launch: partial sums + (last block) dgamma / dbeta / the two apply coefficients
-            L.call("yms_bn_act_bwd_reduce_finalize", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
-                   base + self.sh, base + self.mi, self.act, ws, rt.cnt(self.cnt), rt.pgrad(self.pg),
-                   rt.pgrad(self.pb), coef, rt.st)
-        else:
-            L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
-                   base + self.sh, base + self.mi, self.act, ws, rt.st)
-            L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix,
-                   rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+               base + self.sh, base + self.mi, self.act, ws, rt.st)
+        L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix,
+               rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
         if self.stem_input is not None:
             # the stem's input needs no gradient: the apply pass is fused into the weight
             # gradient, which reads gy, z and the NCHW input.
@@ -369,7 +356,7 @@ class ConvOp:
             # weight gradients -- the two then overlap instead of queueing (step tail 0.53 ms).
             dw = rt.pgrad(self.pw)
             if dw is not None:
-                st = rt.st if os.environ.get("YMS_STEM_WG_SIDE", "0") == "0" else rt.wst()
+                st = rt.st
                 xs = rt.stem_x[self.stem_input]
                 L.call("yms_conv_stem_wgrad", self.sp, xs.data_ptr(), gy, gyl, gyo, z, self.zld, 0, base + self.sc,
                        base + self.sh, base + self.mi, coef, self.act,
@@ -378,10 +365,7 @@ class ConvOp:
             return
         gres = rt.g(r) if r is not None else None
         gro = (r.buf.ld, r.off) if r is not None else (0, 0)
-        # dz overwrites z in place -- unless the depthwise consumer forms act(BN(z)) itself: its
-        # weight gradient (side stream) may still be reading z, so dz goes to the activation
-        # buffer it never materialised (same layout: fresh buffer, ld = r8(c), offset 0)
-        dz = rt.a(y) if self.bnin_by is not None else z
+        dz = z                   # dz overwrites z in place
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
                base + self.sh, base + self.mi, coef, self.act, dz, self.zld, 0, gres, gro[0], gro[1], self.acc_res,
                rt.st)
@@ -414,8 +398,6 @@ class BiasConvOp:
         self.pbias = b.param(conv, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
-        self.red_rows = 0        # > 0: its BN-backward partial rows come from its consumer's dgrad
-        self.bnin_by = None      # depthwise consumer that forms act(BN(z)) itself (no affine pass)
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -496,8 +478,6 @@ class DWConvOp(ConvOp):
         self.pb = b.param(mod.bn, "bias")
         self.flops = 0          # not an MFMA contraction: excluded from the conv roofline
         self.dw_flops = 2 * self.npix * c * k * k
-        self.bnred = None       # producer ConvOp whose BN-backward reduce is fused into this dgrad
-        self.bnin = None        # producer ConvOp whose act(BN(z)) this op forms from z (fwd, wgrad)
         self.pro_by = None      # consumer conv that forms (and stores) this op's output in its prologue
 
     def layout(self, plan, La, Le):
@@ -519,10 +499,6 @@ class DWConvOp(ConvOp):
             # on every call, so a recomputed size could outgrow the region reserved here
             self.wg_ws = L.lib().yms_dwconv_wgrad_ws_bytes(self.sp)
             plan.need_scratch("wgrad", self.wg_ws)
-            self.cnt = plan.counter()
-            if self.bnred is not None:
-                self.bnred.red_rows = L.lib().yms_dwconv_dgrad_rows(self.sp)
-                plan.need_scratch("bwd", 4 * 2 * c * self.bnred.red_rows)
 
     def pack_specs(self):
         return []
@@ -543,13 +519,8 @@ class DWConvOp(ConvOp):
             return
         base = rt.base
         stats = base + rt.plan.scratch["stats"]
-        if self.bnin is not None:
-            p = self.bnin
-            L.call("yms_dwconv_fwd_bnin", self.sp, base + p.z, p.zld, 0, base + p.sc, base + p.sh, p.act, w,
-                   base + self.z, self.zld, 0, stats, self.stats_ld, rt.st)
-        else:
-            L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, base + self.z, self.zld, 0, None, None,
-                   L.ACT_NONE, stats, self.stats_ld, rt.st)
+        L.call("yms_dwconv_fwd", self.sp, rt.a(x), x.buf.ld, x.off, w, base + self.z, self.zld, 0, None, None,
+               L.ACT_NONE, stats, self.stats_ld, rt.st)
         bn = self.mod.bn
         L.call("yms_bn_finalize", self.c, stats, self.stats_rows, self.stats_ld, self.npix, bn.weight.data_ptr(),
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
@@ -572,24 +543,13 @@ class DWConvOp(ConvOp):
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, rt.g(y), y.buf.ld, y.off, base + self.sc,
                base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, None, 0, 0, 0, rt.st)
         w = self.mod.conv.weight.data_ptr()
-        if x.buf.needs_grad and self.bnred is not None:
-            # dx is the producer's whole activation gradient: its BN-backward partial sums come out
-            # of the same pass (the producer's finalize reads them from the "bwd" scratch next)
-            p = self.bnred
-            L.call("yms_dwconv_dgrad_bnred", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off,
-                   base + p.z, p.zld, 0, base + p.sc, base + p.sh, base + p.mi, p.act, ws, rt.st)
-        elif x.buf.needs_grad:
+        if x.buf.needs_grad:
             L.call("yms_dwconv_dgrad", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             wsz = self.wg_ws
-            if self.bnin is not None:
-                p = self.bnin
-                L.call("yms_dwconv_wgrad_bnin", self.sp, base + p.z, p.zld, 0, base + p.sc, base + p.sh, p.act, z,
-                       self.zld, 0, rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
-            else:
-                L.call("yms_dwconv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
-                       rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
+            L.call("yms_dwconv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
+                   rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
 
 
 class AddOp:
@@ -766,7 +726,6 @@ class Plan:
         self.scratch_req = {}
         self.n_counters = 0
         self.stem_inputs = self._find_stems()
-        self._find_dw_bnred()
         self._find_pro()
         La, Le = Layout(), Layout()
         for buf in self.bufs:
@@ -795,11 +754,6 @@ class Plan:
                 if isinstance(y, View) and not any(y is o for o in self.outputs):
                     _check_not_in_place(op, y)
                     T.release(y)
-            for op in self.ops:
-                if getattr(op, "bnred", None) is not None and op.acc_x:
-                    # the fused dgrad stores: keep the separate reduce if dx must accumulate
-                    op.bnred.red_rows = 0
-                    op.bnred = None
             self.gzero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.idx in T.zero]
             self.gzero_ranges.append((self.gscratch["cnt"], 16 * max(self.n_counters, 1)))
         self.flops = sum(op.flops for op in self.ops)
@@ -836,42 +790,6 @@ class Plan:
                 out[i] = op
         return out
 
-    def _find_dw_bnred(self):
-        """Depthwise convs whose input is the whole output of the Conv op right before them and is
-        read by nothing else (the MS-Block IB: 1x1 expand -> BN -> SiLU -> depthwise): the
-        depthwise dgrad writes that activation gradient in full, so it also produces the expand
-        conv's BN-backward partial sums (yms_dwconv_dgrad_bnred) and the expand conv skips its
-        reduce pass; and (BNIN) the depthwise forward and weight gradient form act(BN(z)) of the
-        expand conv from its z while staging, so the expand conv's affine_act pass goes.  Both are
-        opt-in (YMS_DW_BNRED=1, YMS_DW_BNIN=1), measured slower on YOLO-MS-S (interleaved, one box):
-        BNRED 37.06 -> 37.6 ms (the fused dgrad runs at half occupancy; the reduce it replaces
-        re-read data still in the MALL), BNIN 38.24 -> 38.72 ms (affine -0.87 ms, but the
-        converting forward +0.33 ms, the out-of-place dz apply +0.8 ms and the converting weight
-        gradient +2.1 ms on the side stream).  16-bit training only."""
-        bnred = os.environ.get("YMS_DW_BNRED", "0") == "1"
-        bnin = os.environ.get("YMS_DW_BNIN", "0") == "1"
-        if not self.training or self.dt == L.F32 or not (bnred or bnin):
-            return
-        for i, d in enumerate(self.ops):
-            if type(d) is not DWConvOp or i == 0:
-                continue
-            p, x = self.ops[i - 1], d.x
-            if type(p) is not ConvOp or p.stem_input is not None or p.y.buf is not x.buf:
-                continue
-            if p.y.off != x.off or p.y.c != x.c or x.off != 0 or x.buf.zero or not x.buf.needs_grad:
-                continue
-            if any(x.buf is o.buf for o in self.outputs):
-                continue
-            readers = [op for op in self.ops if op is not p
-                       and any(isinstance(a, View) and a.buf is x.buf for a in vars(op).values())]
-            if readers != [d] or p.res is not None or x.buf.ld != r8(p.c):
-                continue
-            if bnred:
-                d.bnred = p
-            if bnin:
-                d.bnin = p
-                p.bnin_by = d
-
     def _find_pro(self):
         """Training, 16-bit: a Conv op whose input view is exactly the output of one earlier Conv /
         depthwise op (no residual in that op's affine pass) and which is the FIRST reader of it
@@ -880,21 +798,17 @@ class Plan:
         tiles, so the producer's affine pass goes (its write stays, its read of z is the conv's own
         input read).  x is still materialised, so every later reader and the whole backward are
         unchanged.  Stride-1 'same' consumers only (their centre tap covers every input pixel once).
-        Opt-in (YMS_PRO=1: 1x1 consumers; YMS_PRO=3: also 3x3): the bytes it removes (the affine
-        pass's z read) do not pay for the prologue conv's lower occupancy -- interleaved on one box,
-        YOLOv8-s 18.36 vs 18.38 ms/step and YOLO-MS-S 35.83 vs 36.75 ms/step, off vs 1x1 on
-        (profiles/r04q_pro_1x1_ab.txt)."""
+        Opt-in (YMS_PRO=1), 1x1 consumers only (3x3 consumers transform every input element once
+        per tap: YOLOv8-s 18.8 -> 20.5 ms/step with them, profiles/r04c_pro_ab.txt): the bytes it
+        removes (the affine pass's z read) do not pay for the prologue conv's lower occupancy --
+        interleaved on one box, YOLOv8-s 18.36 vs 18.38 ms/step and YOLO-MS-S 35.83 vs 36.75 ms/step,
+        off vs on (profiles/r04q_pro_1x1_ab.txt)."""
         if not self.training or self.dt == L.F32 or os.environ.get("YMS_PRO", "0") == "0":
             return
         for i, c in enumerate(self.ops):
             if type(c) is not ConvOp or c.stem_input is not None:
                 continue
             if not L.lib().yms_conv_fwd_pro_supported(c.sp):
-                continue
-            # 3x3 consumers transform every input element once per tap (im2col A tiles): measured
-            # slower than the affine pass they replace (YOLOv8-s 18.8 -> 20.5 ms/step with them,
-            # profiles/r04c_pro_ab.txt); YMS_PRO=3 includes them (dev A/B)
-            if c.shape.k != 1 and os.environ.get("YMS_PRO", "0") != "3":
                 continue
             x = c.x
             prod = None
@@ -909,7 +823,7 @@ class Plan:
             j, q = prod
             if type(q) not in (ConvOp, DWConvOp) or q.y.off != x.off or q.y.c != x.c or q.res is not None:
                 continue
-            if getattr(q, "bnin_by", None) is not None or q.pro_by is not None or q.act not in (L.ACT_NONE, L.ACT_SILU):
+            if q.pro_by is not None or q.act not in (L.ACT_NONE, L.ACT_SILU):
                 continue
             if getattr(q, "stem_input", None) is not None:
                 continue

@@ -125,23 +125,10 @@ WGRAD_SIDE_STREAM = os.environ.get("YMS_WGRAD_STREAM", "1") != "0"
 _SIDE = {}
 
 
-# YMS_SIDE_CUS=k: the side stream may only use k CUs (YMS_SIDE_CU_MODE 0 lowest ids / 1 spread)
-SIDE_CUS = int(os.environ.get("YMS_SIDE_CUS", "0"))
-SIDE_CU_MODE = int(os.environ.get("YMS_SIDE_CU_MODE", "1"))
-
-
 def _side_stream(dev):
     s = _SIDE.get(dev)
     if s is None:
-        if SIDE_CUS > 0:
-            import ctypes
-            with torch.cuda.device(dev):
-                h = ctypes.c_void_p()
-                L.call("yms_stream_create_cu_subset", SIDE_CUS, SIDE_CU_MODE, ctypes.byref(h))
-                s = torch.cuda.ExternalStream(h.value, device=dev)
-        else:
-            s = torch.cuda.Stream(device=dev)
-        _SIDE[dev] = s
+        s = _SIDE[dev] = torch.cuda.Stream(device=dev)
     return s
 
 
@@ -159,8 +146,7 @@ class _PlanFn(torch.autograd.Function):
         rt = Rt(plan, arena.data_ptr(), stream, True)
         _load_inputs(plan, rt, inputs)
         ops = plan.ops
-        if (WGRAD_SIDE_STREAM and os.environ.get("YMS_PACK_SIDE", "1") != "0" and plan.ops
-                and plan.ops[0] in plan.stem_inputs.values()):
+        if WGRAD_SIDE_STREAM and plan.ops and plan.ops[0] in plan.stem_inputs.values():
             # the stem conv reads the fp32 weight itself: the step's weight packs go to the side
             # stream and overlap it; every later conv is ordered after them
             main, side = torch.cuda.current_stream(dev), _side_stream(dev)
