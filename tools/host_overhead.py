@@ -41,3 +41,27 @@ torch.cuda.synchronize()
 t2 = time.perf_counter()
 print(f"host enqueue per step {sum(host) / N * 1e3:.2f} ms (min {min(host) * 1e3:.2f}), "
       f"wall per step {(t2 - t0) / N * 1e3:.2f} ms, queue drained {(t2 - t1) * 1e3:.1f} ms after the last enqueue")
+
+# per phase: host time to enqueue, and GPU time between events recorded at the phase boundaries
+ph = {k: [] for k in ("fwd", "loss", "bwd", "opt")}
+gp = {k: [] for k in ph}
+for _ in range(N):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(5)]
+    opt.zero_grad(set_to_none=True)
+    a = time.perf_counter(); ev[0].record()
+    outs = m(x)
+    b = time.perf_counter(); ev[1].record()
+    loss = crit.loss_tensor(outs, tg)[0]
+    c = time.perf_counter(); ev[2].record()
+    loss.backward()
+    d = time.perf_counter(); ev[3].record()
+    opt.step()
+    e = time.perf_counter(); ev[4].record()
+    for k, (u, v) in zip(ph, ((a, b), (b, c), (c, d), (d, e))):
+        ph[k].append(v - u)
+    torch.cuda.synchronize()
+    for i, k in enumerate(ph):
+        gp[k].append(ev[i].elapsed_time(ev[i + 1]))
+print("phase   host_ms  gpu_ms (median of %d)" % N)
+for k in ph:
+    print(f"{k:5s} {sorted(ph[k])[N // 2] * 1e3:8.2f} {sorted(gp[k])[N // 2]:8.2f}")

@@ -471,6 +471,69 @@ __device__ void sort8192(uint64_t* keys, int n) {
   __syncthreads();
 }
 
+// Ascending merge sort of keys[0, n), n <= 8192, by one 1024-thread block, for the window-grid
+// kernel: each thread sorts 8 consecutive keys in registers (bitonic network), then log2(N2 / 8)
+// merge levels ping-pong between `keys` and `tmp` (both with room for 8192 entries): thread t
+// produces outputs [8t, 8t + 8) of its pair of runs by a merge-path binary search on its
+// diagonal and 8 sequential merge steps.  O(n log n) LDS traffic where the bitonic network of
+// sort8192 makes 91 exchange passes; result in keys[0, n), ends with a barrier.  Padding = ~0
+// (keys are unique, so only pads compare equal).
+__device__ void msort8192(uint64_t* keys, uint64_t* tmp, int n) {
+  const int tid = threadIdx.x;
+  int N2 = 8;
+  while (N2 < n) N2 <<= 1;
+  const bool act = 8 * tid < N2;
+  if (act) {
+    uint64_t r[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int e = 8 * tid + i;
+      r[i] = e < n ? keys[e] : ~0ull;
+    }
+    cas_in_thread<1>(r);
+    cas_in_thread<3>(r);
+    cas_in_thread<1>(r);
+    cas_in_thread<7>(r);
+    cas_in_thread<2>(r);
+    cas_in_thread<1>(r);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) keys[8 * tid + i] = r[i];   // the thread's own 8 slots: no hazard
+  }
+  __syncthreads();
+  uint64_t* src = keys;
+  uint64_t* dst = tmp;
+  for (int L = 8; L < N2; L <<= 1) {
+    if (act) {
+      const int d0 = 8 * tid;
+      const int base = d0 & ~(2 * L - 1), d = d0 - base;
+      const uint64_t* x = src + base;
+      const uint64_t* y = x + L;
+      int lo = max(0, d - L), hi = min(d, L);
+      while (lo < hi) {            // smallest i with x[i] >= y[d - i - 1]
+        const int mid = (lo + hi) >> 1;
+        if (x[mid] < y[d - mid - 1]) lo = mid + 1; else hi = mid;
+      }
+      int i = lo, j = d - lo;
+      uint64_t xv = i < L ? x[i] : ~0ull, yv = j < L ? y[j] : ~0ull;
+      uint64_t o[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const bool tx = j >= L || (i < L && xv < yv);
+        o[k] = tx ? xv : yv;
+        if (tx) { ++i; xv = i < L ? x[i] : ~0ull; } else { ++j; yv = j < L ? y[j] : ~0ull; }
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) dst[d0 + k] = o[k];
+    }
+    __syncthreads();
+    uint64_t* t = src; src = dst; dst = t;
+  }
+  if (src != keys) {
+    for (int e = tid; e < n; e += 1024) keys[e] = src[e];
+    __syncthreads();
+  }
+}
+
 // Segments of more than 8192 keys: 8192-key chunks are sorted by sort8192 in parallel blocks
 // (nms_chunk_sort_kernel, one block per (segment, chunk)), then nms_big_sort_kernel merges the
 // sorted runs pairwise by merge path (each of the 1024 threads finds its split of the output
@@ -1307,6 +1370,8 @@ constexpr int NMS_WG_CELLS = NMS_WG_GMAX * NMS_WG_GMAX;
 constexpr size_t NMS_WG_LDS = (size_t)NMS_WG_MAX * 16 + (size_t)NMS_WG_MAX * 4 + (size_t)(NMS_WG_CELLS + 1) * 8 +
                               (size_t)(NMS_WG_MAX / 32) * 4;
 
+static_assert(NMS_WG_MAX * 16 + NMS_WG_MAX * 4 >= 2 * 8192 * 8, "msort8192 scratch inside s_box / s_items / s_kept");
+
 __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const float* bxy, float thr_f, float tr,
                                                          int gmin, int maxc, int wg_on, NmsWs ws) {
   extern __shared__ float4 s_box[];                                   // [NMS_WG_MAX] sorted boxes
@@ -1318,12 +1383,12 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
   uint32_t* s_alive = reinterpret_cast<uint32_t*>(s_cur + NMS_WG_CELLS + 1);
   __shared__ float s_red[7][16];
   __shared__ int s_wsum[16];
-  __shared__ int s_bad, s_nk, s_nwk, s_cut;
+  __shared__ int s_bad, s_nk, s_nwk, s_cut, s_m;
   __shared__ int s_wk[64], s_win[64];
   __shared__ unsigned long long s_wm[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 #ifdef YMS_NMS_PROF
-  long long wacc[5] = {0, 0, 0, 0, 0}, wpt = 0;
+  long long wacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wpt = 0;
   int nwin = 0;
 #define WMARK(k) do { if (tid == 0) { const long long q_ = clock64(); wacc[k] += q_ - wpt; wpt = q_; } } while (0)
 #else
@@ -1422,6 +1487,7 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         continue;
       }
     }
+    WMARK(7);
     // sort the keys in LDS (priority order), then the sorted anchors to idx and boxes to s_box
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1429,7 +1495,14 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
       if (i < n) s_keys[i] = kv[k];
     }
     __syncthreads();
-    sort8192(s_keys, n);                              // ends with a barrier
+    // merge sort with the region behind the keys as scratch (the rest of s_box, s_items and
+    // s_kept: 64 KB, none of it live before the binning)
+    msort8192(s_keys, s_keys + 8192, n);              // ends with a barrier (bitonic: +21 us per call)
+#ifdef YMS_NMS_PROF
+    WMARK(3);
+    const long long sortc = wacc[3];
+    wacc[3] = 0;
+#endif
     uint32_t av[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1499,60 +1572,68 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
     if (tid == 0) s_cut = -1;
     __syncthreads();
     WMARK(1);
-    const int nwords = (n + 31) >> 5;                 // <= NMS_WG_MAX / 32 = 224 < 1024
+    const int nwords = (n + 31) >> 5;                 // <= NMS_WG_MAX / 32 = 224 <= 4 * 64
     for (;;) {
-      // window: the first 64 alive boxes after the cursor (block-wide scan of the alive words)
-      const int cut0 = s_cut;
-      uint32_t word = 0u;
-      if (tid < nwords) {
-        word = s_alive[tid];
-        const int lo = cut0 + 1;                      // first index still to take
-        if ((tid + 1) * 32 <= lo) word = 0u;
-        else if (tid * 32 < lo) word &= ~0u << (lo - tid * 32);
-      }
-      const int pc = __popc(word);
-      int incl = pc;
+      // 1. window (wave 0 alone, no cross-wave scan): the first 64 alive boxes after the cursor;
+      //    lane l holds alive word w0 + l, 64 words (2048 boxes) at a time from the cursor's word
+      if (wave == 0) {
+        const int lo = s_cut + 1;                     // first index still to take
+        int got = 0;
+        for (int w0 = lo >> 5; w0 < nwords && got < 64; w0 += 64) {   // wave-uniform
+          const int w = w0 + lane;
+          uint32_t v = w < nwords ? s_alive[w] : 0u;
+          if (w * 32 < lo) v &= ~0u << (lo - w * 32);   // only the cursor's word is partial
+          const int pc = __popc(v);
+          int incl = pc;
 #pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        const int v = __shfl_up(incl, o);
-        if (lane >= o) incl += v;
+          for (int o = 1; o < 64; o <<= 1) {
+            const int u = __shfl_up(incl, o);
+            if (lane >= o) incl += u;
+          }
+          int pos = got + incl - pc;
+          while (v && pos < 64) {
+            const int bit = __ffs(v) - 1;
+            v &= v - 1u;
+            s_win[pos++] = w * 32 + bit;
+          }
+          got += __shfl(incl, 63);
+        }
+        if (lane == 0) s_m = min(64, got);
       }
-      if (lane == 63 && wave < 4) s_wsum[wave] = incl;
       __syncthreads();
-      int wb = 0, tot = 0;
-      for (int w = 0; w < 4; ++w) { if (w < wave) wb += s_wsum[w]; tot += s_wsum[w]; }
-      const int m = min(64, tot);
+      const int m = __builtin_amdgcn_readfirstlane(s_m);
       if (m == 0) break;                              // block-uniform
 #ifdef YMS_NMS_PROF
       ++nwin;
 #endif
+      WMARK(4);
+      // 2. pairwise suppression bits of the window, one ballot per row: s_wm[t] bit l = member t
+      //    (higher priority) suppresses member l > t; each lane's own member box loaded once
       {
-        int pos = wb + incl - pc;
-        uint32_t wv = word;
-        while (wv && pos < 64) {
-          const int bit = __ffs(wv) - 1;
-          wv &= wv - 1u;
-          s_win[pos++] = tid * 32 + bit;
+        const float4 bl = s_box[s_win[lane < m ? lane : 0]];
+        for (int t = wave; t < m; t += 16) {
+          const float4 bt = s_box[s_win[t]];
+          const bool hit = lane > t && lane < m && iou_gt_f(bt, bl, thr_f, false);
+          const unsigned long long row = __ballot(hit);
+          if (lane == 0) s_wm[t] = row;
         }
       }
       __syncthreads();
-      // pairwise suppression bits of the window, one ballot per row: s_wm[t] bit l = member t
-      // (higher priority) suppresses member l > t
-      for (int t = wave; t < m; t += 16) {
-        const float4 bt = s_box[s_win[t]];
-        const bool hit = lane > t && lane < m && iou_gt_f(bt, s_box[s_win[lane < m ? lane : 0]], thr_f, false);
-        const unsigned long long row = __ballot(hit);
-        if (lane == 0) s_wm[t] = row;
-      }
-      __syncthreads();
+      WMARK(6);
+      // 3. serial greedy on the bit rows (wave 0, scalar), visiting only the members still alive:
+      //    row t clears bits above t only, so jumping to the next alive member is the same walk
       if (wave == 0) {
         const int i = lane < m ? s_win[lane] : 0;
         const unsigned long long rowl = lane < m ? s_wm[lane] : 0ull;
         unsigned long long alive = m == 64 ? ~0ull : ((1ull << m) - 1ull);
-        for (int t = 0; t < m; ++t) {                 // serial greedy on the bit rows (SALU)
-          const unsigned long long rt = ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(rowl >> 32), t) << 32) |
-                                        (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowl, t);
-          if ((alive >> t) & 1ull) alive &= ~rt;
+        unsigned long long cur = alive;
+        while (cur) {
+          const int t = __builtin_ctzll(cur);
+          const unsigned long long rt =
+              ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(rowl >> 32), t) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowl, t);
+          alive &= ~rt;
+          cur = alive & ~((2ull << t) - 1ull);
         }
         const bool kept = (alive >> lane) & 1ull;
         const int pos = __popcll(alive & ((1ull << lane) - 1ull));
@@ -1569,6 +1650,11 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
       }
       __syncthreads();
       WMARK(2);
+      // 4. every window survivor clears the alive bit of each later box of its search rectangle it
+      //    suppresses; two candidates per lane and step, loads of both issued before either test
+      //    (round 5, measured and dropped: the rectangle's rows flattened into one candidate index
+      //    space, 4 per lane -- 200 -> 230 us per call: the per-candidate row selection costs more
+      //    than the latency it hides)
       const int nwk = s_nwk, cut = s_cut;
       for (int k = wave; k < nwk; k += 16) {
         const int u = s_wk[k];
@@ -1578,10 +1664,15 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         gr_region(g, bu, tr, x0, x1, y0, y1);
         for (int cy = y0; cy <= y1; ++cy) {
           const int plo = s_cst[cy * g.gx + x0], phi = s_cst[cy * g.gx + x1 + 1];
-          for (int p = plo + lane; p < phi; p += 64) {
-            const int j = s_items[p];
-            if (j > cut && ((s_alive[j >> 5] >> (j & 31)) & 1u) && iou_gt_f(bu, s_box[j], thr_f, false))
-              atomicAnd(&s_alive[j >> 5], ~(1u << (j & 31)));
+          for (int p = plo + lane; p < phi; p += 128) {
+            const bool v2 = p + 64 < phi;
+            const int j1 = s_items[p], j2 = v2 ? s_items[p + 64] : j1;
+            const uint32_t a1 = s_alive[j1 >> 5], a2 = s_alive[j2 >> 5];
+            const float4 q1 = s_box[j1], q2 = s_box[j2];
+            if (j1 > cut && ((a1 >> (j1 & 31)) & 1u) && iou_gt_f(bu, q1, thr_f, false))
+              atomicAnd(&s_alive[j1 >> 5], ~(1u << (j1 & 31)));
+            if (v2 && j2 > cut && ((a2 >> (j2 & 31)) & 1u) && iou_gt_f(bu, q2, thr_f, false))
+              atomicAnd(&s_alive[j2 >> 5], ~(1u << (j2 & 31)));
           }
         }
       }
@@ -1605,10 +1696,12 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
       }
     }
 #ifdef YMS_NMS_PROF
-    if (tid == 0 && b < 2)
-      printf("WGRIDPROF b=%d c=%d n=%d kept=%d windows=%d gx=%d gy=%d load=%lld bin=%lld resolve=%lld suppress=%lld compact=%lld\n",
-             b, c, n, s_nk, nwin, g.gx, g.gy, wacc[0], wacc[1], wacc[2], wacc[3], wacc[4]);
-    for (int k = 0; k < 5; ++k) wacc[k] = 0;
+    if (tid == 0 && b < 2) {
+      printf("WGRIDPROF b=%d c=%d n=%d kept=%d windows=%d gx=%d gy=%d load=%lld bin=%lld window=%lld bits=%lld serial=%lld suppress=%lld\n",
+             b, c, n, s_nk, nwin, g.gx, g.gy, wacc[0], wacc[1], wacc[4], wacc[6], wacc[2], wacc[3]);
+      printf("WGRIDPROF2 b=%d c=%d route=%lld sort=%lld\n", b, c, wacc[7], sortc);
+    }
+    for (int k = 0; k < 8; ++k) wacc[k] = 0;
 #endif
     if (tid == 0) {
       ws.cls_cnt[(long)b * nc + c] = s_nk;
@@ -2021,6 +2114,9 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
   if (A > cap || graph) {            // big-path segments exist only then (bucket: route 3)
     const int full = iou < 0.0 ? 1 : 0;
     const unsigned segs = (unsigned)std::min(256, n * nc);
+    // (the kernels after the window-grid greedy usually find no work and exit: ~4.7 us each
+    // whatever their grid -- 64-512 blocks measured the same, profiles/r05n_nms_ab.txt)
+    const unsigned rest = segs;
     // the search radius' threshold, a little below thr_f (slack for the rounding of the bound)
     const float tr = std::max(0.0f, thr_f * (1.0f - 1e-4f) - 1e-6f);
     // 1. route + sort + window-grid greedy in one block per segment (finite segments of <= 8192
@@ -2042,12 +2138,12 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     // 3. the rest (route 3): sorted, then the kept-list greedy
     if (A > NMS_CHUNK)
       hipLaunchKernelGGL(nms_chunk_sort_kernel, dim3(256), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc, w);
-    hipLaunchKernelGGL(nms_big_sort_kernel, dim3(segs), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc,
+    hipLaunchKernelGGL(nms_big_sort_kernel, dim3(rest), dim3(1024), (size_t)NMS_CHUNK * 8, st, A, nc,
                        boxes_xyxy, w);
     // the window-grid greedy over global memory for sorted finite segments of NMS_WG_MAX..NMS_WGG_MAX
     if (!full && wg_on && A > NMS_WG_MAX)
-      hipLaunchKernelGGL(nms_wgrid_glb_kernel, dim3(segs), dim3(1024), 0, st, A, nc, thr_f, tr, w);
-    hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(segs), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
+      hipLaunchKernelGGL(nms_wgrid_glb_kernel, dim3(rest), dim3(1024), 0, st, A, nc, thr_f, tr, w);
+    hipLaunchKernelGGL(nms_big_greedy_kernel, dim3(rest), dim3(1024), NMS_GREEDY_LDS, st, A, nc,
                        thr_f, full, w);
   }
   yms_status e = launch_status();
