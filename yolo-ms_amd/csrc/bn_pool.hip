@@ -248,6 +248,15 @@ __device__ __forceinline__ void load_params8(const float* p, int c0, int c, floa
 // U pixels per thread per iteration: all U loads issue before any use (memory-level
 // parallelism; these kernels are HBM-bound).
 constexpr int BN_U = 4;
+// the backward reduce / apply passes (dev A/B builds; at 8 the YOLOv8-s step went 17.80 -> 17.90 ms
+// (reduce) and -> 19.43 ms (apply), profiles/r05u_bn_unroll_ab.txt)
+#ifndef YMS_BN_UR
+#define YMS_BN_UR 4
+#endif
+#ifndef YMS_BN_UA
+#define YMS_BN_UA 4
+#endif
+constexpr int BN_UR = YMS_BN_UR, BN_UA = YMS_BN_UA;
 
 // Pixel-range order of the elementwise passes over a tensor: blocks are dispatched in index order,
 // so block b taking range nblocks - 1 - b walks the tensor from its end.  A pass that follows one
@@ -396,28 +405,28 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
         a2[i] += da * xh;
       }
     };
-    const long step = (long)m.PY * BN_U;
+    const long step = (long)m.PY * BN_UR;
     if (PIPE && c % 8 == 0) {
       // software-pipelined: the next U pixels' loads are in flight while this U's math runs
       // (2 blocks per CU leave too few waves to hide HBM latency otherwise).  Loads are
       // unconditional -- pixels past the range re-read the last one and are masked out of the
       // sums -- so no branch separates a load from its wait and vmcnt can count.
-      auto issue = [&](long b, Raw8<T> (&g)[BN_U], Raw8<T> (&zz)[BN_U]) {
+      auto issue = [&](long b, Raw8<T> (&g)[BN_UR], Raw8<T> (&zz)[BN_UR]) {
 #pragma unroll
-        for (int u = 0; u < BN_U; ++u) {
+        for (int u = 0; u < BN_UR; ++u) {
           const long pix = min(b + (long)u * m.PY, p1 - 1);
           load_raw8(gy + pix * gy_ld + gy_off + c0, 8, g[u]);
           if (HAS_Z) load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
         }
       };
-      auto consume = [&](long b, const Raw8<T> (&g)[BN_U], const Raw8<T> (&zz)[BN_U]) {
+      auto consume = [&](long b, const Raw8<T> (&g)[BN_UR], const Raw8<T> (&zz)[BN_UR]) {
 #pragma unroll
-        for (int u = 0; u < BN_U; ++u)
+        for (int u = 0; u < BN_UR; ++u)
           if (b + (long)u * m.PY < p1) accum(g[u], zz[u]);
       };
       long base = p0 + m.py;
       if (base < p1) {
-        Raw8<T> ga[BN_U], za[BN_U], gb[BN_U], zb[BN_U];
+        Raw8<T> ga[BN_UR], za[BN_UR], gb[BN_UR], zb[BN_UR];
         issue(base, ga, za);
         while (true) {
           issue(base + step, gb, zb);
@@ -432,9 +441,9 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
       }
     } else {
       for (long base = p0 + m.py; base < p1; base += step) {
-        Raw8<T> gr[BN_U], zr[BN_U];
+        Raw8<T> gr[BN_UR], zr[BN_UR];
 #pragma unroll
-        for (int u = 0; u < BN_U; ++u) {
+        for (int u = 0; u < BN_UR; ++u) {
           const long pix = base + (long)u * m.PY;
           if (pix < p1) {
             load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
@@ -442,7 +451,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
           }
         }
 #pragma unroll
-        for (int u = 0; u < BN_U; ++u)
+        for (int u = 0; u < BN_UR; ++u)
           if (base + (long)u * m.PY < p1) accum(gr[u], zr[u]);
       }
     }
@@ -626,27 +635,27 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
     }
     store8(dz + pix * dz_ld + dz_off + c0, valid, out);
   };
-  const long step = (long)m.PY * BN_U;
+  const long step = (long)m.PY * BN_UA;
   if (PIPE && c % 8 == 0) {
-    auto issue = [&](long b, Raw8<T> (&g)[BN_U], Raw8<T> (&zz)[BN_U], Raw8<T> (&rres)[BN_U]) {
+    auto issue = [&](long b, Raw8<T> (&g)[BN_UA], Raw8<T> (&zz)[BN_UA], Raw8<T> (&rres)[BN_UA]) {
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
+      for (int u = 0; u < BN_UA; ++u) {
         const long pix = min(b + (long)u * m.PY, p1 - 1);
         load_raw8(gy + pix * gy_ld + gy_off + c0, 8, g[u]);
         load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
         if (racc) load_raw8(gres + pix * gres_ld + gres_off + c0, 8, rres[u]);
       }
     };
-    auto consume = [&](long b, const Raw8<T> (&g)[BN_U], const Raw8<T> (&zz)[BN_U], const Raw8<T> (&rres)[BN_U]) {
+    auto consume = [&](long b, const Raw8<T> (&g)[BN_UA], const Raw8<T> (&zz)[BN_UA], const Raw8<T> (&rres)[BN_UA]) {
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
+      for (int u = 0; u < BN_UA; ++u) {
         const long pix = b + (long)u * m.PY;
         if (pix < p1) emit(pix, g[u], zz[u], rres[u], 8);
       }
     };
     long base = p0 + m.py;
     if (base < p1) {
-      Raw8<T> ga[BN_U], za[BN_U], ra[BN_U], gb[BN_U], zb[BN_U], rb[BN_U];
+      Raw8<T> ga[BN_UA], za[BN_UA], ra[BN_UA], gb[BN_UA], zb[BN_UA], rb[BN_UA];
       issue(base, ga, za, ra);
       // the next group's loads go out before this group's stores.  Every pixel is loaded and
       // stored by one thread (in-place dz over z is per pixel and per thread); a clamped load of
@@ -664,9 +673,9 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
     }
   } else {
     for (long base = p0 + m.py; base < p1; base += step) {
-      Raw8<T> gr[BN_U], zr[BN_U], rr[BN_U];
+      Raw8<T> gr[BN_UA], zr[BN_UA], rr[BN_UA];
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
+      for (int u = 0; u < BN_UA; ++u) {
         const long pix = base + (long)u * m.PY;
         if (pix < p1) {
           load_raw8(gy + pix * gy_ld + gy_off + c0, nv, gr[u]);
@@ -675,7 +684,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
         }
       }
 #pragma unroll
-      for (int u = 0; u < BN_U; ++u) {
+      for (int u = 0; u < BN_UA; ++u) {
         const long pix = base + (long)u * m.PY;
         if (pix < p1) emit(pix, gr[u], zr[u], rr[u], nv);
       }
@@ -1082,7 +1091,7 @@ yms_status yms_bn_act_bwd_apply(int dtype, long npix, int c, const void* z, int 
   // software-pipelined loop at eight U-pixel iterations per thread (half the blocks of the serial
   // loop's best, four): YOLO-MS-S 37.27 -> 37.11 ms/step, YOLOv8-s 18.53 -> 18.49 ms (means of
   // two interleaved runs; 4 / 16 iterations pipelined are slower, profiles/r03zf_bn_apply_pipe_ab.txt)
-  const long ppb = elem_ppb(npix, c, 8);
+  const long ppb = elem_ppb(npix, c, 8 * BN_U / BN_UA);    // the same pixels per block at any U
   const unsigned blocks = (unsigned)((npix + ppb - 1) / ppb);
   YMS_DT_DISPATCH(dtype, T, hipLaunchKernelGGL((bn_bwd_apply_kernel<T, true>), dim3(blocks), dim3(256), 0,
                                                (hipStream_t)stream, npix, c, (const T*)z, z_ld, z_off,
