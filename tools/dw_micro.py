@@ -13,6 +13,8 @@ if os.environ.get("YMS_MICRO_SHAPES") == "k9":
 if os.environ.get("YMS_MICRO_SHAPES") == "mss":   # YOLO-MS-S depthwise layers at B=64 (x2, x2, x2, x2, x4, x4)
     SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9),
               (64, 80, 80, 384, 3), (64, 40, 40, 768, 3)]
+if os.environ.get("YMS_MICRO_SHAPES") == "k79":   # VERDICT r04 item 6 shapes (YOLO-MS-S calibrated + round 3)
+    SHAPES = [(64, 40, 40, 288, 7), (64, 20, 20, 288, 9), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9)]
 if os.environ.get("YMS_MICRO_SHAPES") == "mss4":   # round-4 YOLO-MS-S (calibrated) + the round-3 k >= 5 shapes
     SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 160, 5), (64, 40, 40, 288, 7), (64, 20, 20, 288, 9),
               (64, 80, 80, 320, 3), (64, 40, 40, 576, 3), (64, 40, 40, 320, 3), (64, 20, 20, 576, 3),
