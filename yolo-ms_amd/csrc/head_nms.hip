@@ -83,33 +83,14 @@ __global__ __launch_bounds__(256) void head_decode_kernel(DecodeParams p) {
     const float bw = (b0 - a0) * st, bh = (b1 - a1) * st;
     float* o = p.out + t * (4 + p.nc);
     if (sub == 0) { o[0] = cx; o[1] = cy; o[2] = bw; o[3] = bh; }
-    // classes; best = (max prob, first index)
+    // classes: lane `sub` handles c = sub + 16k; best = (max prob, first index)
     float best = -1.0f;
     int bl = 0x7fffffff;
     const T* cls = src + 64;
-    if (p.nc % 8 == 0 && (reinterpret_cast<uintptr_t>(p.out) & 15) == 0) {
-      // lane `sub` owns classes 8 (sub + 16k) .. + 7: one 16-B logit load and two 16-B stores per
-      // 8 classes (output rows are 16-B aligned: (4 + nc) % 4 == 0); same per-element formula
-      for (int c0 = 8 * sub; c0 < p.nc; c0 += 128) {
-        float v[8];
-        Vec8<T>::load(cls + c0, v);
-        float pr[8];
-#pragma unroll
-        for (int i = 0; i < 8; ++i) {
-          pr[i] = 1.0f / (1.0f + expf(-v[i]));
-          if (pr[i] > best) { best = pr[i]; bl = c0 + i; }
-        }
-        float4* o4 = reinterpret_cast<float4*>(o + 4 + c0);
-        o4[0] = make_float4(pr[0], pr[1], pr[2], pr[3]);
-        o4[1] = make_float4(pr[4], pr[5], pr[6], pr[7]);
-      }
-    } else {
-      // lane `sub` handles c = sub + 16k
-      for (int c = sub; c < p.nc; c += 16) {
-        const float pr = 1.0f / (1.0f + expf(-(float)cls[c]));
-        o[4 + c] = pr;
-        if (pr > best) { best = pr; bl = c; }
-      }
+    for (int c = sub; c < p.nc; c += 16) {
+      const float pr = 1.0f / (1.0f + expf(-(float)cls[c]));
+      o[4 + c] = pr;
+      if (pr > best) { best = pr; bl = c; }
     }
     if (p.score) {
 #pragma unroll
