@@ -51,31 +51,35 @@ __global__ __launch_bounds__(256) void head_decode_kernel(DecodeParams p) {
     const int r = a - p.aoff[l];
     const int y = r / p.w[l], x = r - (r / p.w[l]) * p.w[l];
     const T* src = reinterpret_cast<const T*>(p.lvl[l]) + (((long)b * p.h[l] + y) * p.w[l] + x) * p.no_ld;
-    float dist = 0.f;
-    if (sub < 4) {
-      float v[16], vv[8];
-      Vec8<T>::load(src + 16 * sub, vv);
+    // DFL over all 16 lanes: lane sub = 4 side + q owns bins 4q .. 4q + 3 of side `side`; the
+    // softmax max / sums combine over the side's 4 lanes by xor shuffles (every lane busy, where one
+    // lane per side walking 16 bins left 12 of 16 idle through the exponentials)
+    const int side = sub >> 2, q4 = sub & 3;
+    float dist;
+    {
+      float v[4];
 #pragma unroll
-      for (int i = 0; i < 8; ++i) v[i] = vv[i];
-      Vec8<T>::load(src + 16 * sub + 8, vv);
-#pragma unroll
-      for (int i = 0; i < 8; ++i) v[8 + i] = vv[i];
-      float m = v[0];
-#pragma unroll
-      for (int i = 1; i < 16; ++i) m = fmaxf(m, v[i]);
+      for (int i = 0; i < 4; ++i) v[i] = (float)src[16 * side + 4 * q4 + i];
+      float m = fmaxf(fmaxf(v[0], v[1]), fmaxf(v[2], v[3]));
+      m = fmaxf(m, __shfl_xor(m, 1, 16));
+      m = fmaxf(m, __shfl_xor(m, 2, 16));
       float s = 0.f, e = 0.f;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) {
+      for (int i = 0; i < 4; ++i) {
         const float ex = expf(v[i] - m);
         s += ex;
-        e += ex * (float)i;
+        e += ex * (float)(4 * q4 + i);
       }
+      s += __shfl_xor(s, 1, 16);
+      e += __shfl_xor(e, 1, 16);
+      s += __shfl_xor(s, 2, 16);
+      e += __shfl_xor(e, 2, 16);
       dist = e / s;
     }
-    // gather the 4 distances (lanes 0..3 of this 16-lane group)
+    // gather the 4 distances (lane 4 k of this 16-lane group holds side k's)
     const int base = (threadIdx.x & 63) & ~15;
-    const float d0 = __shfl(dist, base + 0), d1 = __shfl(dist, base + 1);
-    const float d2 = __shfl(dist, base + 2), d3 = __shfl(dist, base + 3);
+    const float d0 = __shfl(dist, base + 0), d1 = __shfl(dist, base + 4);
+    const float d2 = __shfl(dist, base + 8), d3 = __shfl(dist, base + 12);
     const float ax = (float)x + 0.5f, ay = (float)y + 0.5f, st = p.stride[l];
     const float a0 = ax - d0, a1 = ay - d1;
     const float b0 = ax + d2, b1 = ay + d3;
