@@ -2,8 +2,9 @@
 // NHWC, the large-kernel mid conv of the YOLO-MS MS-Block inverted bottleneck (SURVEY 7.4:
 // IB_k = 1x1 expand -> depthwise k x k -> 1x1 project; heterogeneous kernel sizes 3/5/7/9 per
 // backbone stage, the "HKS" of the paper; the reference holds the MS-Block only as a diagram,
-// annotations.md:66-133).  Not a dense contraction: VALU + LDS, bounded by HBM (k = 3, 5) or
-// by the VALU FMA rate (k = 7, 9), never MFMA.
+// annotations.md:66-133).  Forward / dgrad: VALU + LDS, bounded by HBM (k = 3, 5) or by the VALU
+// FMA rate (k = 7, 9); the k = 5 / 7 / 9 weight gradient on maps up to 64 wide runs on MFMA as a
+// band-diagonal product (dwconv_wgrad_mfma_kernel).
 //
 // Mapping: a 256-thread block owns a TY x TX = 8 x 32 output tile of one image and 32 channels;
 // wave w owns 8 channels (one 16-B NHWC chunk), lane (ty, qx) = (lane / 8, lane % 8) owns the
@@ -24,6 +25,8 @@
 namespace yms {
 
 constexpr int DW_TY = 8, DW_TX = 32, DW_RX = 4, DW_G = 4, DW_CB = DW_G * 8;   // 32 channels per block
+constexpr int DW_FEW_ROWS = 32;   // weight-gradient partial rows summed by the one-pass reduce
+constexpr int DW_WGM_CG = 16;     // channels per dwconv_wgrad_mfma_kernel block
 enum { DW_FWD_AFFINE = 0, DW_FWD_STATS = 1, DW_DGRAD = 2 };
 
 struct DwParams {
@@ -42,7 +45,21 @@ struct DwParams {
   int N, H, W, C;
   int tiles_x, tiles_y;  // spatial tiles per image
   int ysplit, tps;       // forward / dgrad: strips per image column of tiles, tiles per strip
+  int ncg, nlog;         // strip kernels: channel groups, logical blocks (see dw_block)
 };
+
+// logical (spatial block bx, channel group by) of a strip kernel's 1-D launch: channel groups
+// fastest and the grid padded to a multiple of 8 so consecutive logical blocks run on one XCD
+// (block i runs on XCD i % 8) -- the channel groups of one tile read the same 128-B lines of each
+// NHWC pixel through one L2, instead of each group streaming the whole map separately (a map larger
+// than the 256-MB Infinity Cache was then fetched from HBM once per group)
+__device__ __forceinline__ bool dw_block(const DwParams& p, int& bx, int& by) {
+  const int l = (int)((blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3));
+  if (l >= p.nlog) return false;
+  by = l % p.ncg;
+  bx = l / p.ncg;
+  return true;
+}
 
 // LDS row stride (16-B chunks) for rows of n chunks: one chunk of padding when n is a multiple
 // of 4 (a 64-B multiple: rows read by one wave's lanes would start in the same banks); other
@@ -162,11 +179,13 @@ void dwconv_kernel(DwParams p) {
   float (*wl)[K * K][8] = reinterpret_cast<float (*)[K * K][8]>(smem + RING_B);
   float (*scl)[16] = reinterpret_cast<float (*)[16]>(smem + RING_B + WL_B);   // eval scale | shift (LDS:
                                                                                 // not live across the FMAs)
+  int bx, by;
+  if (!dw_block(p, bx, by)) return;
   const int per_img = p.tiles_x * p.ysplit;
-  const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
+  const int n = bx / per_img, sidx = bx - n * per_img;
   const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
   const int x0 = tx * TX;
-  const int c0 = blockIdx.y * CB;
+  const int c0 = by * CB;
   {
     // the block's 32 x K x K weights are one contiguous range of p.w: coalesced loads, all issued
     // before the LDS stores (dgrad correlates with the kernel rotated by 180 degrees)
@@ -340,7 +359,7 @@ void dwconv_kernel(DwParams p) {
       const uint32_t so = (uint32_t)(((long)tile * 2 * p.stats_ld + c + lane) * 4);
       dw_bst4(rstat, sok ? so : NT_OOB, a);
       dw_bst4(rstat, sok ? so + (uint32_t)p.stats_ld * 4u : NT_OOB, b);
-      dw_bst4(rcnt, (blockIdx.y == 0 && threadIdx.x == 0) ? (uint32_t)tile * 4u : NT_OOB, (float)(vy * vx));
+      dw_bst4(rcnt, (by == 0 && threadIdx.x == 0) ? (uint32_t)tile * 4u : NT_OOB, (float)(vy * vx));
     }
     wait_vmcnt<NST>();
     __syncthreads();
@@ -612,11 +631,13 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
   constexpr int RING_B = G * RB * RS * (int)sizeof(Raw8<T>);
   __shared__ __attribute__((aligned(16))) char smem[RING_B];
   Raw8<T>* ring = reinterpret_cast<Raw8<T>*>(smem);
+  int bx, by;
+  if (!dw_block(p, bx, by)) return;
   const int per_img = p.tiles_x * p.ysplit;
-  const int n = blockIdx.x / per_img, sidx = blockIdx.x - n * per_img;
+  const int n = bx / per_img, sidx = bx - n * per_img;
   const int tx = sidx % p.tiles_x, t0 = (sidx / p.tiles_x) * p.tps, t1 = min(p.tiles_y, t0 + p.tps);
   const int x0 = tx * TX;
-  const int c0 = blockIdx.y * CB;
+  const int c0 = by * CB;
   const int g = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const int ty = lane / CGX, qx = lane - ty * CGX;
   const int c = c0 + 8 * g, nv = min(8, p.C - c);
@@ -711,13 +732,246 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
   if (lane == 0 && nv > 0) {
 #pragma unroll
     for (int t = 0; t < K * K; ++t) {
-      float* o = ws + ((long)blockIdx.x * K * K + t) * p.C + c;
+      float* o = ws + ((long)bx * K * K + t) * p.C + c;
       *reinterpret_cast<f32x4*>(o) = f32x4{part[t / K][t % K][0], part[t / K][t % K][1], part[t / K][t % K][2],
                                            part[t / K][t % K][3]};
       *reinterpret_cast<f32x4*>(o + 4) = f32x4{part[t / K][t % K][4], part[t / K][t % K][5],
                                                part[t / K][t % K][6], part[t / K][t % K][7]};
     }
   }
+}
+
+// wgrad, k = 5 / 7 / 9 on maps at most 64 wide, 16-bit types: the per-channel correlation on MFMA.
+// For one channel, rows a of the padded input and rows b of dz,
+//   G_dx[a][b] = sum_x Xp[a][x + dx] D[b][x],   dw[dy][dx] = sum_b G_dx[b + dy][b]
+// i.e. per kernel column dx one product (a x x) . (x x b) whose band diagonals a - b = 0 .. K-1 are
+// the weight gradient.  A unit = (image, 16 dz rows b0 .. b0 + 15): the band a - b in [0, K) lies in
+// two 16 x 16 blocks, the diagonal one (a in b0 .. b0 + 15) and the one below it (a in b0 + 16 ..
+// b0 + 31, skipped when those rows are all padding), each accumulated over 32-column chunks by
+// mfma_f32_16x16x32 into per-(block, dx) accumulators that stay in registers across all of a thread
+// block's units (the diagonals are relative to b0).  Of the lower block only rows a < b0 + 16 + K - 1
+// reach the band: the rest of its rows are whatever LDS holds there, and their products land in
+// entries a - b >= K that are never read.  The dz fragment (lane: row b, 8 columns) is read once per
+// chunk and reused by 2 K products; the input fragment (lane: row a, 16 columns) once per block and
+// chunk, the K column windows dx = 0 .. K-1 cut from registers (dword selects / v_alignbit).  At the
+// end each wave sums the 16 entries of every diagonal through LDS in a fixed order and writes
+// ws[group][t][c]; a reduce kernel sums the groups.  LDS holds a unit channel-major (8 channels:
+// 16 + K - 1 input rows, 16 dz rows; image column x of the input at x + 4), rows 96 / 160 B apart: the
+// 16 rows one ds_read_b128 lane group touches (two column slots) fall in distinct banks.  Staging
+// items are 4 pixels x 8 channels of one row: four 16-B raw-buffer loads (out-of-image pixels read
+// as zeros through the range check), re-paired per channel with v_perm into eight 8-B LDS writes;
+// the next unit's items are loaded into registers while the current one computes.
+template <int K, int NCH, int CG>
+struct DwWgM {
+  static constexpr int P = K / 2, PA = 4, SH = PA - P, XR = 16 + K - 1, NT = 32 * CG, NW = CG / 2, H2 = CG / 8;
+  static constexpr int XL = NCH == 1 ? 48 : 80;                  // row stride (elements) = both operands'
+  static constexpr int XE = CG * XR * XL, LDS_EL = XE + CG * 16 * XL;
+  static constexpr int NIX = (XR * 8 * NCH * H2 + NT - 1) / NT, NID = (16 * 8 * NCH * H2 + NT - 1) / NT;
+  static_assert(XL >= 32 * NCH + 8, "row holds the chunks and the window overhang");
+  static_assert(LDS_EL * 2 <= (CG == 8 ? 80 : 160) * 1024 && NW * 512 * 4 <= LDS_EL * 2, "LDS");
+};
+
+template <typename T> __device__ __forceinline__ f32x4 mfma16x16x32(const u32x4& a, const u32x4& b, f32x4 c);
+template <> __device__ __forceinline__ f32x4 mfma16x16x32<bf16>(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), __builtin_bit_cast(bf16x8, b), c, 0, 0,
+                                                 0);
+}
+template <> __device__ __forceinline__ f32x4 mfma16x16x32<f16>(const u32x4& a, const u32x4& b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(f16x8, a), __builtin_bit_cast(f16x8, b), c, 0, 0, 0);
+}
+// 8 consecutive 16-bit values starting at element s of a 16-element register row
+__device__ __forceinline__ u32x4 dw_window(const unsigned (&v)[8], int s) {
+  const int m = s >> 1;
+  if (!(s & 1)) return u32x4{v[m], v[m + 1], v[m + 2], v[m + 3]};
+  return u32x4{__builtin_amdgcn_alignbit(v[m + 1], v[m], 16), __builtin_amdgcn_alignbit(v[m + 2], v[m + 1], 16),
+               __builtin_amdgcn_alignbit(v[m + 3], v[m + 2], 16), __builtin_amdgcn_alignbit(v[m + 4], v[m + 3], 16)};
+}
+template <typename T, int K, int NCH, int CG>
+__global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_kernel(DwParams p, const char* dz,
+                                                                                   int dz_ld, int dz_off, float* ws,
+                                                                                   int nj, int upb, int ncg, int ngrp) {
+  using G = DwWgM<K, NCH, CG>;
+  constexpr int P = G::P, PA = G::PA, SH = G::SH, XR = G::XR, XL = G::XL, NT = G::NT, NW = G::NW, H2 = G::H2;
+  constexpr int NIX = G::NIX, NID = G::NID;
+  __shared__ __attribute__((aligned(16))) unsigned short lds[G::LDS_EL];
+  unsigned short* xs = lds;
+  unsigned short* ds = lds + G::XE;
+  // block -> (unit group, channel group), channel group fastest.  The grid is padded to a multiple
+  // of 8 and block i runs on XCD i % 8: consecutive logical blocks (the channel groups of the same
+  // pixels, 2 CG B of each 128-B line apiece) run on one XCD and share its L2
+  const int b = (blockIdx.x & 7) * (gridDim.x >> 3) + (blockIdx.x >> 3);
+  if (b >= ncg * ngrp) return;
+  const int cgi = b % ncg, grp = b / ncg;
+  const int c0 = cgi * CG;
+  const int u0 = grp * upb, u1 = min(p.N * nj, u0 + upb);
+  const int tid = threadIdx.x;
+  // staging items: (row, group of 4 columns, 8-channel half), halves fastest (neighbouring lanes
+  // load the two 16-B halves of one pixel's 32 B).  Per item: LDS offset of its first channel's row
+  // segment, byte offset of its first pixel in image row 0 (-1: no item / channels past C), the
+  // staged row, and how many of its 4 pixels lie inside the map
+  const int ng = (p.W + 3) >> 2;
+  const uint32_t xrow = (uint32_t)p.W * p.src_ld * 2, drow = (uint32_t)p.W * dz_ld * 2;
+  int xslot[NIX], xoff[NIX], xr_[NIX], xm[NIX], dslot[NID], doff[NID], dr_[NID], dm[NID];
+#pragma unroll
+  for (int i = 0; i < NIX; ++i) {
+    const int it = tid + NT * i, h = it % H2, rm = it / H2, r = rm / ng, m = rm - r * ng;
+    const bool ok = r < XR && c0 + 8 * h < p.C;
+    xslot[i] = (8 * h * XR + r) * XL + 4 * m + PA;
+    xoff[i] = ok ? (int)((((uint32_t)r * p.W + 4 * m) * p.src_ld + 8 * h) * 2) : -1;
+    xr_[i] = r;
+    xm[i] = ok ? min(4, p.W - 4 * m) : 0;
+  }
+#pragma unroll
+  for (int i = 0; i < NID; ++i) {
+    const int it = tid + NT * i, h = it % H2, rm = it / H2, r = rm / ng, m = rm - r * ng;
+    const bool ok = r < 16 && c0 + 8 * h < p.C;
+    dslot[i] = (8 * h * 16 + r) * XL + 4 * m;
+    doff[i] = ok ? (int)((((uint32_t)r * p.W + 4 * m) * dz_ld + 8 * h) * 2) : -1;
+    dr_[i] = r;
+    dm[i] = ok ? min(4, p.W - 4 * m) : 0;
+  }
+  // columns outside the image, past the map width and channels past C stay zero for every unit
+  for (int i = tid; i < G::LDS_EL / 8; i += NT) reinterpret_cast<u32x4*>(lds)[i] = u32x4{0u, 0u, 0u, 0u};
+  const char* xsrc = reinterpret_cast<const char*>(reinterpret_cast<const T*>(p.src) + p.src_off + c0);
+  const char* dsrc = reinterpret_cast<const char*>(reinterpret_cast<const T*>(dz) + dz_off + c0);
+  const long ximg = (long)p.H * p.W * p.src_ld * 2, dimg = (long)p.H * p.W * dz_ld * 2;
+  u32x4 xv[NIX][4], dv[NID][4];
+  // rows outside the image load as zeros (the LDS rows vary per unit); pixels past the map width
+  // are never loaded (their LDS columns stay zero)
+  auto load = [&](int unit) {
+    const int n = unit / nj, j = unit - n * nj;
+    const char* xi = xsrc + n * ximg;
+    const char* di = dsrc + n * dimg;
+    const int yx = 16 * j - P, yd = 16 * j;   // image row of staged row 0
+#pragma unroll
+    for (int i = 0; i < NIX; ++i) {
+      const int y = yx + xr_[i];
+      const bool ok = xoff[i] >= 0 && y >= 0 && y < p.H;
+      const uint32_t o = (uint32_t)xoff[i] + (uint32_t)yx * xrow;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        xv[i][k] = u32x4{0u, 0u, 0u, 0u};
+        if (ok && k < xm[i]) xv[i][k] = *reinterpret_cast<const u32x4*>(xi + o + k * p.src_ld * 2);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NID; ++i) {
+      const int y = yd + dr_[i];
+      const bool ok = doff[i] >= 0 && y < p.H;
+      const uint32_t o = (uint32_t)doff[i] + (uint32_t)yd * drow;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        dv[i][k] = u32x4{0u, 0u, 0u, 0u};
+        if (ok && k < dm[i]) dv[i][k] = *reinterpret_cast<const u32x4*>(di + o + k * dz_ld * 2);
+      }
+    }
+  };
+  // 4 pixels x 8 channels -> 8 channel rows of 4 columns (one 8-B write each)
+  auto put = [&](unsigned short* d0, int cs, const u32x4 (&v)[4]) {
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const unsigned lo01 = __builtin_amdgcn_perm(v[1][d], v[0][d], 0x05040100u);
+      const unsigned lo23 = __builtin_amdgcn_perm(v[3][d], v[2][d], 0x05040100u);
+      const unsigned hi01 = __builtin_amdgcn_perm(v[1][d], v[0][d], 0x07060302u);
+      const unsigned hi23 = __builtin_amdgcn_perm(v[3][d], v[2][d], 0x07060302u);
+      *reinterpret_cast<uint2*>(d0 + (2 * d) * cs) = make_uint2(lo01, lo23);
+      *reinterpret_cast<uint2*>(d0 + (2 * d + 1) * cs) = make_uint2(hi01, hi23);
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < NIX; ++i)
+      if (xoff[i] >= 0) put(xs + xslot[i], XR * XL, xv[i]);
+#pragma unroll
+    for (int i = 0; i < NID; ++i)
+      if (doff[i] >= 0) put(ds + dslot[i], 16 * XL, dv[i]);
+  };
+  const int lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  f32x4 acc[2][2][K];   // [channel of the wave][diagonal / lower block][dx]
+#pragma unroll
+  for (int cl = 0; cl < 2; ++cl)
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int dx = 0; dx < K; ++dx) acc[cl][s][dx] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int unit) {
+    const int j = unit % nj;
+    const bool lower = 16 * j + 16 - P < p.H;   // the lower block's input rows are not all padding
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+      const int ch = w + NW * cl;
+#pragma unroll
+      for (int q = 0; q < NCH; ++q) {
+        const u32x4 bw = *reinterpret_cast<const u32x4*>(ds + (ch * 16 + r16) * XL + 32 * q + 8 * g);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) {
+          if (s == 1 && !lower) break;
+          const unsigned short* xr = xs + (ch * XR + 16 * s + r16) * XL + 32 * q + 8 * g;
+          const u32x4 v0 = *reinterpret_cast<const u32x4*>(xr), v1 = *reinterpret_cast<const u32x4*>(xr + 8);
+          const unsigned v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+          for (int dx = 0; dx < K; ++dx) acc[cl][s][dx] = mfma16x16x32<T>(dw_window(v, dx + SH), bw, acc[cl][s][dx]);
+        }
+      }
+    }
+  };
+  // LDS-only barriers: __syncthreads() would drain the next unit's loads (vmcnt(0)) right after
+  // issuing them
+  if (u0 < u1) load(u0);
+  for (int unit = u0; unit < u1; ++unit) {
+    lds_barrier();   // zero fill done / the previous unit's reads done
+    store();
+    if (unit + 1 < u1) load(unit + 1);
+    lds_barrier();
+    compute(unit);
+  }
+  // diagonal sums: lane (b = lane & 15, a = 4 (lane >> 4) + i) holds G[a][b] (diagonal block) and
+  // G[a + 16][b] (lower block); dw[dy][dx] = sum over b of G[b + dy][b], 16 terms in a fixed order
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(lds) + w * 512;
+#pragma unroll
+  for (int cl = 0; cl < 2; ++cl) {
+    const int c = c0 + w + NW * cl;
+#pragma unroll
+    for (int dx = 0; dx < K; ++dx) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        red[(4 * g + i) * 16 + r16] = acc[cl][0][dx][i];
+        red[256 + (4 * g + i) * 16 + r16] = acc[cl][1][dx][i];
+      }
+      __syncthreads();
+      // lane (dy = lane & 15, quarter h = lane >> 4) sums b = 4 h .. 4 h + 3, then the quarters pair up
+      const int dy = r16;
+      float sum = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int bb = 4 * g + k;
+        sum += bb + dy < 16 ? red[(bb + dy) * 16 + bb] : red[256 + ((bb + dy) & 15) * 16 + bb];
+      }
+      sum += __shfl_xor(sum, 16);
+      sum += __shfl_xor(sum, 32);
+      if (g == 0 && dy < K && c < p.C) ws[((long)grp * K * K + dy * K + dx) * p.C + c] = sum;
+      __syncthreads();
+    }
+  }
+}
+
+// dw[c][t] (+)= sum_b ws[b][t][c] for few rows (the MFMA kernel's unit groups): one output per
+// thread, rows summed in order with all loads in flight
+__global__ __launch_bounds__(256) void dwconv_wgrad_reduce_few_kernel(const float* ws, int blocks, int C, int KK,
+                                                                      float* dw, int accumulate) {
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const long stride = (long)C * KK;
+  if (j >= stride) return;
+  float v[DW_FEW_ROWS];
+#pragma unroll
+  for (int b = 0; b < DW_FEW_ROWS; ++b) v[b] = b < blocks ? ws[(long)b * stride + j] : 0.f;
+  float s = 0.f;
+#pragma unroll
+  for (int b = 0; b < DW_FEW_ROWS; ++b) s += v[b];
+  const int t = j / C, c = j - t * C;
+  float* o = dw + (long)c * KK + t;
+  *o = accumulate ? *o + s : s;
 }
 
 // dw[c][t] (+)= sum_b ws[b][t][c]: 64 outputs per block, 16 waves; wave w sums blocks
@@ -809,6 +1063,13 @@ static dim3 dw_strip_grid(const yms_dw_shape* s, DwParams& p) {
   return dim3((unsigned)((long)s->n * p.tiles_x * p.ysplit), (unsigned)cg);
 }
 
+// the 1-D launch of a strip kernel's (spatial blocks x channel groups) grid (dw_block)
+static dim3 dw_launch(dim3 g, DwParams& p) {
+  p.ncg = (int)g.y;
+  p.nlog = (int)(g.x * g.y);
+  return dim3((unsigned)((p.nlog + 7) / 8 * 8));
+}
+
 static bool dw_shape_ok(const yms_dw_shape* s) {
   return s && s->n > 0 && s->h > 0 && s->w > 0 && s->c > 0 && s->c % 8 == 0 && (s->k == 3 || s->k == 5 || s->k == 7 || s->k == 9) &&
          s->dtype >= 0 && s->dtype <= 2 && (long)s->n * s->h * s->w < (1l << 31);
@@ -858,6 +1119,28 @@ static int dw_wg2_blocks(const yms_dw_shape* s) {
   const long tiles = (long)s->n * ((s->w + tx - 1) / tx) * ((s->h + ty - 1) / ty);
   const int cg = (s->c + DW_CB - 1) / DW_CB;
   return (int)std::max(1l, std::min(tiles, std::max(1l, (long)(2 * conv_cu_count()) / cg)));
+}
+
+// k = 5 / 7 / 9 weight gradient on MFMA (dwconv_wgrad_mfma_kernel): 16-bit types, maps at most 64
+// wide (one or two 32-column chunks per staged row)
+static bool dw_wgm(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32 && s->w <= 64; }
+struct DwWgmCfg {
+  int nch, nj, ncg, upb, groups;
+};
+// units = (image, 16 dz rows); 16 channels per block (512 threads, one block per CU: 8 waves of
+// ~220 VGPRs; 32-B pixel pieces per block, measured 4-8 % faster on k = 7 than 8-channel blocks at
+// two per CU, equal on k = 9); units per block: the fewest that keep the grid within one round of
+// the resident blocks; each unit group adds one ws row per tap and channel
+static DwWgmCfg dw_wgm_cfg(const yms_dw_shape* s) {
+  DwWgmCfg c;
+  c.nch = s->w <= 32 ? 1 : 2;
+  c.nj = (s->h + 15) / 16;
+  c.ncg = (s->c + DW_WGM_CG - 1) / DW_WGM_CG;
+  const long units = (long)s->n * c.nj, slots = (DW_WGM_CG == 8 ? 2l : 1l) * conv_cu_count();
+  c.upb = (int)std::max(1l, (units * c.ncg + slots - 1) / slots);
+  while (c.upb < units && (long)c.ncg * ((units + c.upb - 1) / c.upb) > slots) ++c.upb;
+  c.groups = (int)((units + c.upb - 1) / c.upb);
+  return c;
 }
 
 // spatial partitions of the wgrad grid: about 1024 blocks in total over the channel groups (two
@@ -962,7 +1245,7 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   p.scale = scale; p.shift = shift; p.act = act; p.stats = stats; p.stats_ld = stats_ld;
   if (stats) p.stats_cnt = stats + (long)yms_dwconv_stats_rows(s) * 2 * stats_ld;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  const dim3 grid = dw_strip_grid(s, p);
+  const dim3 grid = dw_launch(dw_strip_grid(s, p), p);
   hipStream_t st = (hipStream_t)stream;
   const int TX = dw_fwd_tx(s);
   if (dw_fwd_g(s) == 8) {
@@ -988,7 +1271,7 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
   p.src = (const char*)dz; p.src_ld = dz_ld; p.src_off = dz_off; p.w = w;
   p.dst = (char*)dx; p.dst_ld = dx_ld; p.dst_off = dx_off; p.accumulate = accumulate;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  const dim3 grid = dw_strip_grid(s, p);
+  const dim3 grid = dw_launch(dw_strip_grid(s, p), p);
   hipStream_t st = (hipStream_t)stream;
   const int TX = dw_fwd_tx(s);
   if (dw_fwd_g(s) == 8) {
@@ -1008,6 +1291,10 @@ size_t yms_dwconv_wgrad_ws_bytes(const yms_dw_shape* s) {
     DwParams p{};
     return (size_t)dw_wg3_grid(s, p).x * row;
   }
+  if (dw_wgm(s)) {
+    const DwWgmCfg c = dw_wgm_cfg(s);
+    return (size_t)c.groups * row;
+  }
   return (size_t)(dw_wg2(s) ? dw_wg2_blocks(s) : dw_wgrad_blocks(s)) * row;
 }
 
@@ -1024,11 +1311,32 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
   int blocks;
   if (dw_wg3(s)) {
     if (!dw_image_fits(s, x_ld)) return YMS_ERR_UNSUPPORTED;
-    const dim3 grid = dw_wg3_grid(s, p);
+    const dim3 g2 = dw_wg3_grid(s, p), grid = dw_launch(g2, p);
     const int TX = dw_fwd_tx(s);
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_wgrad3_kernel<TT, TXX, 4>), grid, dim3(256), 0, st,
                                                            p, (const char*)dz, dz_ld, dz_off, ws)));
-    blocks = (int)grid.x;
+    blocks = (int)g2.x;
+  } else if (dw_wgm(s)) {
+    if (!dw_image_fits(s, x_ld) || !dw_image_fits(s, dz_ld)) return YMS_ERR_UNSUPPORTED;
+    const DwWgmCfg c = dw_wgm_cfg(s);
+    blocks = c.groups;
+    const dim3 grid((unsigned)(((long)c.groups * c.ncg + 7) / 8 * 8));
+#define YMS_DWM_L(KV, NV)                                                                                   \
+  hipLaunchKernelGGL((dwconv_wgrad_mfma_kernel<TT, KV, NV, DW_WGM_CG>), grid, dim3(32 * DW_WGM_CG), 0, st, p,          \
+                     (const char*)dz, dz_ld, dz_off, \
+                     ws, c.nj, c.upb, c.ncg, c.groups)
+    YMS_DW_T16(s->dtype, {
+      if (c.nch == 1) {
+        if (s->k == 5) YMS_DWM_L(5, 1);
+        else if (s->k == 7) YMS_DWM_L(7, 1);
+        else YMS_DWM_L(9, 1);
+      } else {
+        if (s->k == 5) YMS_DWM_L(5, 2);
+        else if (s->k == 7) YMS_DWM_L(7, 2);
+        else YMS_DWM_L(9, 2);
+      }
+    });
+#undef YMS_DWM_L
   } else if (dw_wg2(s)) {
     blocks = dw_wg2_blocks(s);
     const dim3 grid((unsigned)blocks, (unsigned)((s->c + DW_CB - 1) / DW_CB));
@@ -1050,8 +1358,12 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
   }
   yms_status e = launch_status();
   if (e != YMS_OK) return e;
-  hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
-                     blocks, s->c, KK2, dw, accumulate);
+  if (blocks <= DW_FEW_ROWS)
+    hipLaunchKernelGGL(dwconv_wgrad_reduce_few_kernel, dim3((unsigned)((s->c * KK2 + 255) / 256)), dim3(256), 0, st, ws,
+                       blocks, s->c, KK2, dw, accumulate);
+  else
+    hipLaunchKernelGGL(dwconv_wgrad_reduce_kernel, dim3((unsigned)((s->c * KK2 + 63) / 64)), dim3(1024), 0, st, ws,
+                       blocks, s->c, KK2, dw, accumulate);
   return launch_status();
 }
 

@@ -676,13 +676,6 @@ constexpr int NMS_CELLS = NMS_GMAX * NMS_GMAX + 1;
 constexpr size_t NMS_GREEDY_LDS =
     (size_t)NMS_KEPT_LDS * 16 + (size_t)NMS_CELLS * NMS_CELL_CAP * 2 + (size_t)NMS_CELLS * 4;
 
-// Barrier ordering LDS only: outstanding global loads (the next block's candidate prefetch) and
-// stores (kept-list compaction) stay in flight across it, unlike __syncthreads()'s vmcnt(0).
-__device__ __forceinline__ void lds_barrier() {
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
-}
 
 __device__ __forceinline__ int nms_cell(float v, float o, float inv, int g) {
   float f = (v - o) * inv;

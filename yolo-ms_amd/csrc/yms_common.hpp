@@ -89,6 +89,14 @@ __device__ __forceinline__ void store8(T* p, int valid, const float (&v)[8]) {
 
 // 8 channel values kept in their storage format (4 VGPRs for 16-bit types, 8 for fp32) so
 // that several pixels' loads can be in flight per thread without spending 8 VGPRs each.
+// Barrier ordering LDS only: outstanding global loads (register prefetches of later work) and
+// stores stay in flight across it, unlike __syncthreads()'s vmcnt(0).
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 template <typename T> struct Raw8 { u32x4 v[sizeof(T) / 2]; };
 
 template <typename T>
