@@ -3,7 +3,7 @@
 // IB_k = 1x1 expand -> depthwise k x k -> 1x1 project; heterogeneous kernel sizes 3/5/7/9 per
 // backbone stage, the "HKS" of the paper; the reference holds the MS-Block only as a diagram,
 // annotations.md:66-133).  Forward / dgrad: VALU + LDS, bounded by HBM (k = 3, 5) or by the VALU
-// FMA rate (k = 7, 9); the k = 5 / 7 / 9 weight gradient on maps up to 64 wide runs on MFMA as a
+// FMA rate (k = 7, 9); the k = 5 / 7 / 9 weight gradient on maps up to 64 (k = 5: 96) wide runs on MFMA as a
 // band-diagonal product (dwconv_wgrad_mfma_kernel).
 //
 // Mapping: a 256-thread block owns a TY x TX = 8 x 32 output tile of one image and 32 channels;
@@ -741,7 +741,8 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
   }
 }
 
-// wgrad, k = 5 / 7 / 9 on maps at most 64 wide, 16-bit types: the per-channel correlation on MFMA.
+// wgrad, k = 5 / 7 / 9 on maps at most 64 wide (k = 5: 96), 16-bit types: the per-channel correlation
+// on MFMA.
 // For one channel, rows a of the padded input and rows b of dz,
 //   G_dx[a][b] = sum_x Xp[a][x + dx] D[b][x],   dw[dy][dx] = sum_b G_dx[b + dy][b]
 // i.e. per kernel column dx one product (a x x) . (x x b) whose band diagonals a - b = 0 .. K-1 are
@@ -764,7 +765,7 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
 template <int K, int NCH, int CG>
 struct DwWgM {
   static constexpr int P = K / 2, PA = 4, SH = PA - P, XR = 16 + K - 1, NT = 32 * CG, NW = CG / 2, H2 = CG / 8;
-  static constexpr int XL = NCH == 1 ? 48 : 80;                  // row stride (elements) = both operands'
+  static constexpr int XL = NCH == 1 ? 48 : (NCH == 2 ? 80 : 112);   // row stride (elements), both operands'
   static constexpr int XE = CG * XR * XL, LDS_EL = XE + CG * 16 * XL;
   static constexpr int NIX = (XR * 8 * NCH * H2 + NT - 1) / NT, NID = (16 * 8 * NCH * H2 + NT - 1) / NT;
   static_assert(XL >= 32 * NCH + 8, "row holds the chunks and the window overhang");
@@ -1122,8 +1123,11 @@ static int dw_wg2_blocks(const yms_dw_shape* s) {
 }
 
 // k = 5 / 7 / 9 weight gradient on MFMA (dwconv_wgrad_mfma_kernel): 16-bit types, maps at most 64
-// wide (one or two 32-column chunks per staged row)
-static bool dw_wgm(const yms_dw_shape* s) { return s->k >= 5 && s->dtype != YMS_F32 && s->w <= 64; }
+// wide (one or two 32-column chunks per staged row), k = 5 also up to 96 (three chunks: the 2 x 2 x 5
+// accumulators leave registers for them; k = 7 / 9 would spill)
+static bool dw_wgm(const yms_dw_shape* s) {
+  return s->k >= 5 && s->dtype != YMS_F32 && (s->w <= 64 || (s->w <= 96 && s->k == 5));
+}
 struct DwWgmCfg {
   int nch, nj, ncg, upb, groups;
 };
@@ -1133,7 +1137,7 @@ struct DwWgmCfg {
 // the resident blocks; each unit group adds one ws row per tap and channel
 static DwWgmCfg dw_wgm_cfg(const yms_dw_shape* s) {
   DwWgmCfg c;
-  c.nch = s->w <= 32 ? 1 : 2;
+  c.nch = (s->w + 31) / 32;
   c.nj = (s->h + 15) / 16;
   c.ncg = (s->c + DW_WGM_CG - 1) / DW_WGM_CG;
   const long units = (long)s->n * c.nj, slots = (DW_WGM_CG == 8 ? 2l : 1l) * conv_cu_count();
@@ -1330,10 +1334,12 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
         if (s->k == 5) YMS_DWM_L(5, 1);
         else if (s->k == 7) YMS_DWM_L(7, 1);
         else YMS_DWM_L(9, 1);
-      } else {
+      } else if (c.nch == 2) {
         if (s->k == 5) YMS_DWM_L(5, 2);
         else if (s->k == 7) YMS_DWM_L(7, 2);
         else YMS_DWM_L(9, 2);
+      } else {
+        YMS_DWM_L(5, 3);
       }
     });
 #undef YMS_DWM_L
