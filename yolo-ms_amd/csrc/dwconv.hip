@@ -957,6 +957,233 @@ __global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_ke
   }
 }
 
+// forward / dgrad, 16-bit types, on MFMA (selected for k = 7 on maps up to 48 wide: dw_fm): per
+// channel a Toeplitz product per kernel row.  For a block of 16 output rows y0 .. y0 + 15 and 16 output columns x0 .. x0 + 15,
+//   Y[m][n] = sum_dy sum_k A_dy[m][k] B_dy[k][n],  A_dy[m][k] = X[y0 + m + dy - P][x0 + k - 4],
+//   B_dy[k][n] = w[dy][k - n - SH]  (zero outside 0 .. K-1; SH = 4 - P)
+// one mfma_f32_16x16x32 per kernel row over 32 staged columns (the 16 + K - 1 the outputs reach sit
+// inside them).  The weights enter as two bf16 / f16 parts (w = hi + lo, residual 2^-16 |w|), so the
+// products match the fp32-weight VALU kernels to fp32 rounding: two MFMAs per kernel row, still far
+// under the HBM time.  B_dy (per channel, lane: 8 rows k of column n) is built once per block in
+// registers; the input fragment is one ds_read_b128 per (row block, column block, dy).  A block is
+// (image, 16 output rows, 8 channels): the 16 + K - 1 input rows staged channel-major as the
+// MFMA weight gradient stages them (4 pixels x 8 channels per item, v_perm, 8-B LDS writes), 2
+// channels per wave with all ceil(W / 16) column blocks' accumulators in registers; the epilogue
+// (folded BN + SiLU | statistics of the tile | dgrad accumulate) goes back to NHWC through LDS as
+// 16-B pixel chunks.  Statistics rows: one per (image, 16-row block) -- yms_dwconv_stats_rows.
+constexpr int dw_fm_xl(int ncb) {   // row stride: >= 16 ncb + 16 elements, (16-B units) = 2 mod 4
+  int t = (16 * ncb + 16 + 7) / 8;
+  while (t % 4 != 2) ++t;
+  return 8 * t;
+}
+template <int K, int NCB>
+struct DwFm {
+  static constexpr int P = K / 2, SH = 4 - P, XR = 16 + K - 1, XL = dw_fm_xl(NCB), WMAX = 16 * NCB;
+  static constexpr int XE = 8 * XR * XL;                                   // staged input (elements)
+  static constexpr int NI = (XR * (WMAX / 4) + 255) / 256;                 // 4-pixel items per thread
+  static_assert(XE * 2 + 8 * K * K * 4 <= 80 * 1024, "two blocks per CU");
+  static_assert(16 * WMAX * 8 <= XE, "output tile fits the staging area");
+};
+
+template <typename T, int K, int NCB, int MODE>
+__global__ __launch_bounds__(256, 2) void dwconv_mfma_kernel(DwParams p, int upb) {
+  using G = DwFm<K, NCB>;
+  constexpr int P = G::P, SH = G::SH, XR = G::XR, XL = G::XL, NI = G::NI;
+  constexpr bool STATS = MODE == DW_FWD_STATS;
+  __shared__ __attribute__((aligned(16))) unsigned short xs[G::XE];
+  __shared__ float wl[8][K * K];
+  int grp, by;
+  if (!dw_block(p, grp, by)) return;
+  const int nj = (p.H + 15) >> 4;
+  const int u0 = grp * upb, u1 = min(p.N * nj, u0 + upb);
+  const int c0 = 8 * by;
+  const bool cok = c0 < p.C;
+  const int tid = threadIdx.x;
+  // input items: (staged row r, 4-pixel group m), fixed per thread; rows outside the image load as
+  // zeros.  The next unit's items are loaded into registers while the current one computes.
+  const int ng = (p.W + 3) >> 2;
+  const char* src = reinterpret_cast<const char*>(reinterpret_cast<const T*>(p.src) + p.src_off + c0);
+  const long img = (long)p.H * p.W * p.src_ld * 2;
+  int ir[NI], im[NI];
+#pragma unroll
+  for (int i = 0; i < NI; ++i) {
+    const int it = tid + 256 * i;
+    ir[i] = it / ng;
+    im[i] = it - ir[i] * ng;
+  }
+  u32x4 v[NI][4];
+  auto load = [&](int unit) {
+    const int n = unit / nj, y0 = 16 * (unit - n * nj);
+    const char* si = src + n * img;
+#pragma unroll
+    for (int i = 0; i < NI; ++i) {
+      const int y = y0 - P + ir[i];
+      const bool ok = ir[i] < XR && y >= 0 && y < p.H && cok;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[i][k] = u32x4{0u, 0u, 0u, 0u};
+        if (ok && 4 * im[i] + k < p.W)
+          v[i][k] = *reinterpret_cast<const u32x4*>(si + ((long)(y * p.W + 4 * im[i] + k) * p.src_ld) * 2);
+      }
+    }
+  };
+  auto store = [&]() {
+#pragma unroll
+    for (int i = 0; i < NI; ++i)
+      if (ir[i] < XR) {
+        unsigned short* d0 = xs + ir[i] * XL + 4 * im[i] + 4;
+#pragma unroll
+        for (int d = 0; d < 4; ++d) {
+          const unsigned lo01 = __builtin_amdgcn_perm(v[i][1][d], v[i][0][d], 0x05040100u);
+          const unsigned lo23 = __builtin_amdgcn_perm(v[i][3][d], v[i][2][d], 0x05040100u);
+          const unsigned hi01 = __builtin_amdgcn_perm(v[i][1][d], v[i][0][d], 0x07060302u);
+          const unsigned hi23 = __builtin_amdgcn_perm(v[i][3][d], v[i][2][d], 0x07060302u);
+          *reinterpret_cast<uint2*>(d0 + (2 * d) * XR * XL) = make_uint2(lo01, lo23);
+          *reinterpret_cast<uint2*>(d0 + (2 * d + 1) * XR * XL) = make_uint2(hi01, hi23);
+        }
+      }
+  };
+  if (u0 < u1) load(u0);
+  // weights (dgrad: rotated by 180 degrees), channels past C zero
+  for (int it = tid; it < 8 * K * K; it += 256) {
+    const int cl = it / (K * K), t = it - cl * (K * K);
+    const int tw = MODE == DW_DGRAD ? K * K - 1 - t : t;
+    wl[cl][tw] = c0 + cl < p.C ? p.w[(long)(c0 + cl) * K * K + t] : 0.0f;
+  }
+  __syncthreads();
+  const int lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
+  // B_dy fragments of the wave's two channels (rows k = 8 g .. 8 g + 7 of column n = lane & 15), hi
+  // and lo parts, built once for all the block's units
+  u32x4 bh[2][K], bl[2][K];
+  float sc[2], sf[2];
+#pragma unroll
+  for (int cl = 0; cl < 2; ++cl) {
+    const int ch = w + 4 * cl, c = c0 + ch;
+#pragma unroll
+    for (int dy = 0; dy < K; ++dy) {
+      T hv[8], lv[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int dx = 8 * g + e - r16 - SH;
+        const float wv = dx >= 0 && dx < K ? wl[ch][dy * K + dx] : 0.0f;
+        hv[e] = (T)wv;
+        lv[e] = (T)(wv - (float)hv[e]);
+      }
+      __builtin_memcpy(&bh[cl][dy], hv, 16);
+      __builtin_memcpy(&bl[cl][dy], lv, 16);
+    }
+    sc[cl] = 1.f;
+    sf[cl] = 0.f;
+    if (MODE == DW_FWD_AFFINE && c < p.C) {
+      if (p.scale) sc[cl] = p.scale[c];
+      if (p.shift) sf[cl] = p.shift[c];
+    }
+  }
+  // columns outside the image and past the map width stay zero for every unit
+  for (int i = tid; i < G::XE / 8; i += 256) reinterpret_cast<u32x4*>(xs)[i] = u32x4{0u, 0u, 0u, 0u};
+  T* ys = reinterpret_cast<T*>(xs);
+  for (int unit = u0; unit < u1; ++unit) {
+    const int n = unit / nj, y0 = 16 * (unit - n * nj);
+    const int vy = min(16, p.H - y0);
+    lds_barrier();   // zero fill / the previous unit's output stores read
+    if (unit > u0) {
+      // the output tile overwrote the staging area: restore the zero columns
+      for (int i = tid; i < 16 * p.W; i += 256) reinterpret_cast<u32x4*>(xs)[i] = u32x4{0u, 0u, 0u, 0u};
+      lds_barrier();
+    }
+    store();
+    if (unit + 1 < u1) load(unit + 1);
+    lds_barrier();
+    f32x4 acc[2][NCB];
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+      const int ch = w + 4 * cl;
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb) {
+        f32x4 a4 = f32x4{0.f, 0.f, 0.f, 0.f};
+        if (16 * cb < p.W) {
+          const unsigned short* xr = xs + (ch * XR + r16) * XL + 16 * cb + 8 * g;
+#pragma unroll
+          for (int dy = 0; dy < K; ++dy) {
+            const u32x4 av = *reinterpret_cast<const u32x4*>(xr + dy * XL);
+            a4 = mfma16x16x32<T>(av, bh[cl][dy], a4);
+            a4 = mfma16x16x32<T>(av, bl[cl][dy], a4);
+          }
+        }
+        acc[cl][cb] = a4;
+      }
+    }
+    // epilogue.  Lane (column n = lane & 15, rows 4 (lane >> 4) + i) of column block cb holds output
+    // pixel (y0 + 4 g + i, 16 cb + n) of channel c0 + w + 4 cl.
+    lds_barrier();   // staging reads done: the area becomes the [row][column][8 channels] output tile
+#pragma unroll
+    for (int cl = 0; cl < 2; ++cl) {
+      const int chl = w + 4 * cl, c = c0 + chl;
+      if (STATS) {
+        float s = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (4 * g + i < vy && 16 * cb + r16 < p.W) s += acc[cl][cb][i];
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) s += __shfl_xor(s, m);
+        const float mu = s / (float)(vy * p.W);
+        float q = 0.f;
+#pragma unroll
+        for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (4 * g + i < vy && 16 * cb + r16 < p.W) {
+              const float d = acc[cl][cb][i] - mu;
+              q += d * d;
+            }
+#pragma unroll
+        for (int m = 1; m < 64; m <<= 1) q += __shfl_xor(q, m);
+        if (lane == 0 && c < p.C) {
+          p.stats[(long)unit * 2 * p.stats_ld + c] = s;
+          p.stats[(long)unit * 2 * p.stats_ld + p.stats_ld + c] = q;
+        }
+      }
+#pragma unroll
+      for (int cb = 0; cb < NCB; ++cb)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int r = 4 * g + i, x = 16 * cb + r16;
+          if (r < vy && x < p.W) {
+            float o = acc[cl][cb][i];
+            if (MODE == DW_FWD_AFFINE) {
+              o = o * sc[cl] + sf[cl];
+              if (p.act == YMS_ACT_SILU) o = silu_f(o);
+            }
+            ys[(r * p.W + x) * 8 + chl] = (T)o;
+          }
+        }
+    }
+    if (STATS && by == 0 && tid == 0) p.stats_cnt[unit] = (float)(vy * p.W);
+    lds_barrier();
+    // 16-B NHWC stores (dgrad accumulate: + the destination's values in fp32)
+    if (cok) {
+      T* dst = reinterpret_cast<T*>(p.dst) + p.dst_off + c0 + ((long)n * p.H + y0) * p.W * p.dst_ld;
+      for (int it = tid; it < vy * p.W; it += 256) {
+        T* o = dst + (long)it * p.dst_ld;
+        const u32x4 val = *reinterpret_cast<const u32x4*>(ys + it * 8);
+        if (MODE == DW_DGRAD && p.accumulate) {
+          float a[8], b8[8];
+          Vec8<T>::load(o, a);
+          T t8[8];
+          __builtin_memcpy(t8, &val, 16);
+#pragma unroll
+          for (int e = 0; e < 8; ++e) b8[e] = (float)t8[e] + a[e];
+          Vec8<T>::store(o, b8);
+        } else {
+          *reinterpret_cast<u32x4*>(o) = val;
+        }
+      }
+    }
+  }
+}
+
 // dw[c][t] (+)= sum_b ws[b][t][c] for few rows (the MFMA kernel's unit groups): one output per
 // thread, rows summed in order with all loads in flight
 __global__ __launch_bounds__(256) void dwconv_wgrad_reduce_few_kernel(const float* ws, int blocks, int C, int KK,
@@ -1071,6 +1298,21 @@ static dim3 dw_launch(dim3 g, DwParams& p) {
   return dim3((unsigned)((p.nlog + 7) / 8 * 8));
 }
 
+// forward / dgrad on MFMA (dwconv_mfma_kernel): k = 7, 16-bit types, maps up to 48 wide (two or
+// three 16-column blocks).  Measured against the VALU strip kernels on the YOLO-MS shapes
+// (profiles/r05x_dw_fm_ab.txt): k = 7 1.0-1.3x faster (forward with statistics 1.3x); k = 3 / 5 / 9
+// slower or even (per-unit staging and epilogue through LDS bound it, not the MFMAs), so they stay
+// on the VALU kernels.
+static bool dw_fm(const yms_dw_shape* s) { return s->k == 7 && s->dtype != YMS_F32 && s->w <= 48; }
+static int dw_fm_ncb(const yms_dw_shape* s) { return s->w <= 32 ? 2 : 3; }
+// grid: (unit groups, 8-channel groups); units (image, 16 output rows) per block: about two rounds
+// of two resident blocks per CU (the weight fragments are built once per block)
+static dim3 dw_fm_grid(const yms_dw_shape* s, int& upb) {
+  const long units = (long)s->n * ((s->h + 15) / 16), ncg = (s->c + 7) / 8;
+  upb = (int)std::max(1l, (units * ncg + 4l * conv_cu_count() - 1) / (4l * conv_cu_count()));
+  return dim3((unsigned)((units + upb - 1) / upb), (unsigned)ncg);
+}
+
 static bool dw_shape_ok(const yms_dw_shape* s) {
   return s && s->n > 0 && s->h > 0 && s->w > 0 && s->c > 0 && s->c % 8 == 0 && (s->k == 3 || s->k == 5 || s->k == 7 || s->k == 9) &&
          s->dtype >= 0 && s->dtype <= 2 && (long)s->n * s->h * s->w < (1l << 31);
@@ -1169,6 +1411,11 @@ static int dw_wgrad_blocks(const yms_dw_shape* s) {
     else if ((TXV) == 20) { constexpr int TXX = 20; __VA_ARGS__; } \
     else { constexpr int TXX = 32; __VA_ARGS__; }               \
   } while (0)
+#define YMS_DW_NCB(V, ...)                                      \
+  do {                                                          \
+    if ((V) == 2) { constexpr int NCBB = 2; __VA_ARGS__; }      \
+    else { constexpr int NCBB = 3; __VA_ARGS__; }               \
+  } while (0)
 #define YMS_DW_T16(dt, ...)                                     \
   do {                                                          \
     if ((dt) == YMS_BF16) { typedef bf16 TT; __VA_ARGS__; }     \
@@ -1231,6 +1478,7 @@ extern "C" {
 
 int yms_dwconv_stats_rows(const yms_dw_shape* s) {
   if (!dw_shape_ok(s)) return 0;
+  if (dw_fm(s)) return s->n * ((s->h + 15) / 16);
   int tx, ty;
   return dw_fwd_tiles(s, tx, ty);
 }
@@ -1249,8 +1497,17 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
   p.scale = scale; p.shift = shift; p.act = act; p.stats = stats; p.stats_ld = stats_ld;
   if (stats) p.stats_cnt = stats + (long)yms_dwconv_stats_rows(s) * 2 * stats_ld;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  const dim3 grid = dw_launch(dw_strip_grid(s, p), p);
   hipStream_t st = (hipStream_t)stream;
+  if (dw_fm(s)) {
+    int upb;
+    const dim3 grid = dw_launch(dw_fm_grid(s, upb), p);
+    YMS_DW_T16(s->dtype, YMS_DW_NCB(dw_fm_ncb(s), {
+      if (stats) hipLaunchKernelGGL((dwconv_mfma_kernel<TT, 7, NCBB, DW_FWD_STATS>), grid, dim3(256), 0, st, p, upb);
+      else hipLaunchKernelGGL((dwconv_mfma_kernel<TT, 7, NCBB, DW_FWD_AFFINE>), grid, dim3(256), 0, st, p, upb);
+    }));
+    return launch_status();
+  }
+  const dim3 grid = dw_launch(dw_strip_grid(s, p), p);
   const int TX = dw_fwd_tx(s);
   if (dw_fwd_g(s) == 8) {
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
@@ -1275,8 +1532,15 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
   p.src = (const char*)dz; p.src_ld = dz_ld; p.src_off = dz_off; p.w = w;
   p.dst = (char*)dx; p.dst_ld = dx_ld; p.dst_off = dx_off; p.accumulate = accumulate;
   p.N = s->n; p.H = s->h; p.W = s->w; p.C = s->c;
-  const dim3 grid = dw_launch(dw_strip_grid(s, p), p);
   hipStream_t st = (hipStream_t)stream;
+  if (dw_fm(s)) {
+    int upb;
+    const dim3 grid = dw_launch(dw_fm_grid(s, upb), p);
+    YMS_DW_T16(s->dtype, YMS_DW_NCB(dw_fm_ncb(s), hipLaunchKernelGGL((dwconv_mfma_kernel<TT, 7, NCBB, DW_DGRAD>), grid,
+                                                                      dim3(256), 0, st, p, upb)));
+    return launch_status();
+  }
+  const dim3 grid = dw_launch(dw_strip_grid(s, p), p);
   const int TX = dw_fwd_tx(s);
   if (dw_fwd_g(s) == 8) {
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_DGRAD, TXX, 8>), grid, dim3(512), 0,
