@@ -1266,7 +1266,12 @@ static int dw_occ(const yms_dw_shape* s) {
 // channel groups of 8 per forward / dgrad block: 8 (64 channels = one 128-B line of an NHWC pixel
 // per block, 512 threads) for k = 3 when C is a multiple of 64, else 4 (32 channels: the other half
 // of each line is read and written by another block at another time).
-static int dw_fwd_g(const yms_dw_shape* s) { return s->k == 3 && s->c % 64 == 0 && s->dtype != YMS_F32 ? 8 : 4; }
+#ifndef DW_G8_ANY
+#define DW_G8_ANY 0
+#endif
+static int dw_fwd_g(const yms_dw_shape* s) {
+  return s->k == 3 && (s->c % 64 == 0 || (DW_G8_ANY && s->c > 64)) && s->dtype != YMS_F32 ? 8 : 4;
+}
 
 // forward / dgrad grid: image column tiles split into strips of tps tiles.  The strip length is
 // chosen so the blocks fill whole rounds of the resident slots (occupancy x CUs): a block walks its
