@@ -41,6 +41,9 @@ CONFIGS = {
     "halo": {"YMS_WG_HALO": "1", "YMS_WG_RING": "0"},
     "ring": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1"},
     "ringall": {"YMS_WG_HALO": "0", "YMS_WG_RING": "2"},
+    "slab10": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_SLAB_RATIO": "0.1"},
+    "slab20": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_SLAB_RATIO": "0.2"},
+    "slab50": {"YMS_WG_HALO": "1", "YMS_WG_RING": "1", "YMS_WG_SLAB_RATIO": "0.5"},
 }
 sel = os.environ.get("YMS_WGM_CONFIGS")
 if sel:
@@ -60,6 +63,7 @@ for key, cnt in sorted(shapes.items(), key=lambda kv: -kv[0][1] * kv[0][2] * kv[
     flops += fl * cnt
     row = []
     for c, env in CONFIGS.items():
+        os.environ.pop("YMS_WG_SLAB_RATIO", None)
         for a, b in env.items():
             os.environ[a] = b
         wsb = L.lib().yms_conv_wgrad_ws_bytes(sp)
