@@ -19,6 +19,8 @@ if os.environ.get("YMS_MICRO_SHAPES") == "mss4":   # round-4 YOLO-MS-S (calibrat
     SHAPES = [(64, 160, 160, 64, 3), (64, 80, 80, 160, 5), (64, 40, 40, 288, 7), (64, 20, 20, 288, 9),
               (64, 80, 80, 320, 3), (64, 40, 40, 576, 3), (64, 40, 40, 320, 3), (64, 20, 20, 576, 3),
               (64, 80, 80, 128, 5), (64, 40, 40, 256, 7), (64, 20, 20, 512, 9)]
+if os.environ.get("YMS_MICRO_SHAPES") == "k3big":
+    SHAPES = [(64, 160, 160, 64, 3)]
 if os.environ.get("YMS_MICRO_SHAPES") == "msl":   # YOLO-MS-L backbone depthwise layers at B=64 (x4 each)
     SHAPES = [(64, 160, 160, 112, 3), (64, 80, 80, 224, 5), (64, 40, 40, 448, 7), (64, 20, 20, 384, 9),
               (64, 80, 80, 112, 3), (64, 40, 40, 224, 3), (64, 20, 20, 192, 3)]

@@ -8,7 +8,7 @@ order = []
 for f in sorted(glob.glob(os.path.join(d, "p*", "*counter_collection.csv"))):
     for r in csv.DictReader(open(f)):
         name = r["Kernel_Name"]
-        if "conv" not in name and "wgrad" not in name:
+        if "conv" not in name and "wgrad" not in name and "dwconv" not in name:
             continue
         short = name.split("<")[0].replace("void ", "").replace("yms::", "")[:24]
         tmpl = name[name.find("<"):name.find(">") + 1][:40] if "<" in name else ""
