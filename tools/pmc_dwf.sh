@@ -1,4 +1,5 @@
-# Dev: PMC passes over tools/dw_micro.py forward (k3@160 c64) for the default and the all-k MFMA forward build
+# Dev (r05z record): PMC passes over tools/dw_micro.py forward (k3@160 c64) for an all-k MFMA forward build
+# (tools/bin/libyms_fmall.so from a DW_FM_ALL define that was removed after the measurement)
 set -e
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 export YMS_MICRO_SHAPES=k3big YMS_DWM_OPS=fwd
