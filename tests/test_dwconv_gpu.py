@@ -28,7 +28,9 @@ SHAPES = [(2, 20, 20, 64, 3), (1, 17, 33, 48, 5), (3, 40, 40, 32, 7), (2, 13, 9,
           (2, 16, 64, 64, 3), (1, 12, 96, 40, 7), (2, 20, 20, 128, 9),
           (2, 21, 30, 40, 9), (40, 20, 20, 256, 9), (2, 19, 70, 24, 5), (1, 33, 96, 40, 5),
           (2, 18, 28, 48, 7), (16, 40, 40, 256, 7)]
-TOL = {"f32": 2e-5, "bf16": 1e-2}
+TOL = {"f32": 2e-5, "bf16": 1e-2, "f16": 2e-3}
+# f16 through the 16-bit paths (the MFMA kernels' f16 builtins) on the k >= 5 shapes
+F16_SHAPES = [sh for sh in SHAPES if sh[4] >= 5]
 
 
 def _close(got, ref, tol):
@@ -37,8 +39,8 @@ def _close(got, ref, tol):
     assert err <= tol * scale + 1e-6, f"max err {err:.3g} vs scale {scale:.3g} (tol {tol})"
 
 
-@pytest.mark.parametrize("dt", ["f32", "bf16"])
-@pytest.mark.parametrize("shp", SHAPES)
+@pytest.mark.parametrize("dt,shp", [(d, sh) for sh in SHAPES for d in ("f32", "bf16")] +
+                         [("f16", sh) for sh in F16_SHAPES])
 def test_dwconv_fwd_dgrad_wgrad(shp, dt):
     n, h, w, c, k = shp
     dtype = DT[dt]
@@ -86,7 +88,7 @@ def test_dwconv_fwd_dgrad_wgrad(shp, dt):
     dw = torch.full((c, 1, k, k), 0.5, device="cuda")
     L.call("yms_dwconv_wgrad", sp, xb.data_ptr(), xb.shape[-1], 8, dzb.data_ptr(), dzb.shape[-1], 0, ws.data_ptr(),
            wsb, dw.data_ptr(), 1, st)
-    _close(dw.cpu() - 0.5, wg.grad, 1e-4 if dt == "f32" else 2e-3)
+    _close(dw.cpu() - 0.5, wg.grad, {"f32": 1e-4, "bf16": 2e-3, "f16": 5e-4}[dt])
 
 
 def test_add_views():
