@@ -105,3 +105,27 @@ def test_cpu_input_raises():
     from yolov8.model.components import Conv
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         Conv(3, 8)(torch.zeros(1, 3, 8, 8))
+
+
+def test_dwconv_host_sizing_follows_the_kernel_selection():
+    """Depthwise statistics rows and weight-gradient workspace (host functions, no GPU): the k = 7
+    MFMA forward on maps <= 48 wide writes one statistics row per (image, 16-row block); the VALU strip
+    forward one per tile (TX 20 / 40 -> TY 12 / 6); the MFMA weight gradient (16-bit, k >= 5, maps <= 64
+    wide, k = 5 <= 96) sums whole per-group rows of K*K*C floats, few enough for the one-pass reduce."""
+    def sh(n, h, w, c, k, dt):
+        return ctypes.pointer(L.DwShape(n, h, w, c, k, dt))
+    rows = L.lib().yms_dwconv_stats_rows
+    assert rows(sh(64, 40, 40, 288, 7, L.BF16)) == 64 * 3            # MFMA forward: 16-row blocks
+    assert rows(sh(3, 18, 28, 48, 7, L.F16)) == 3 * 2
+    assert rows(sh(64, 40, 40, 288, 7, L.F32)) == 64 * 1 * 7         # fp32 keeps the strip walker
+    assert rows(sh(64, 20, 20, 288, 9, L.BF16)) == 64 * 1 * 2        # k9: strip walker, TX 20 / TY 12
+    assert rows(sh(64, 96, 96, 64, 7, L.BF16)) == 64 * 3 * 12        # > 48 wide: TX 32 / TY 8
+    ws = L.lib().yms_dwconv_wgrad_ws_bytes
+    for (n, h, w, c, k) in ((64, 20, 20, 288, 9), (64, 40, 40, 288, 7), (64, 80, 80, 160, 5), (2, 13, 9, 16, 9)):
+        b = ws(sh(n, h, w, c, k, L.BF16))
+        row = k * k * c * 4
+        assert b > 0 and b % row == 0 and b // row <= 32, (n, h, w, c, k, b // row)
+        units = n * ((h + 15) // 16)
+        assert b // row <= units
+    assert ws(sh(64, 40, 40, 288, 7, L.BF16)) < ws(sh(64, 40, 40, 288, 7, L.F32))   # fp32: tile kernel rows
+    assert ws(sh(2, 13, 9, 12, 9, L.BF16)) == 0                                    # C % 8 != 0: rejected
