@@ -19,8 +19,9 @@ pytestmark = pytest.mark.gpu
 # geometry -- TX 20 (w 20, 9), 40 (33, 40, 80, 23), 32 (70, 45, 64, 96), 64-channel k = 3 blocks
 # (C 64 / 128 / 192), 32-channel blocks for every k; fp32 runs the tile weight-gradient kernel.
 # 16-bit k = 5 / 7 / 9 at widths <= 64 (k = 5: 96) take the MFMA weight gradient: one (w 9, 20, 24,
-# 28, 30), two (33, 40, 45, 50) and three (70, 96) column chunks (each k with one and two), partial channel groups (C 24, 40), partial
-# last row blocks (h 13, 19, 21, 33) and several units per block (n 40).  16-bit k = 7 at widths
+# 28, 30), two (33, 40, 45, 50) and three (70, 96) column chunks (each k with one and two), partial
+# channel groups (C 24, 40), partial last row blocks (h 13, 19, 21, 33) and several units per block
+# (n 40).  16-bit k = 7 at widths
 # <= 48 runs forward / dgrad on MFMA too: two (w 28) and three (40, 45) column blocks, a 2-row last
 # row block (h 18), several units per block (n 16)
 SHAPES = [(2, 20, 20, 64, 3), (1, 17, 33, 48, 5), (3, 40, 40, 32, 7), (2, 13, 9, 16, 9), (1, 80, 80, 64, 9),
