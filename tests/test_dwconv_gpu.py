@@ -20,15 +20,16 @@ pytestmark = pytest.mark.gpu
 # (C 64 / 128 / 192), 32-channel blocks for every k; fp32 runs the tile weight-gradient kernel.
 # 16-bit k = 5 / 7 / 9 at widths <= 64 (k = 5: 96) take the MFMA weight gradient: one (w 9, 20, 24,
 # 28, 30), two (33, 40, 45, 50) and three (70, 96) column chunks (each k with one and two), partial
-# channel groups (C 24, 40), partial last row blocks (h 13, 19, 21, 33) and several units per block
-# (n 40).  16-bit k = 7 at widths
+# channel groups (C 24, 40), partial last row blocks (h 13, 19, 21, 33), several units per block
+# (n 40) and 32-row units for maps of 17-32 rows in one chunk (h 18, 20, 21, 25, 32).  16-bit k = 7 at widths
 # <= 48 runs forward / dgrad on MFMA too: two (w 28) and three (40, 45) column blocks, a 2-row last
 # row block (h 18), several units per block (n 16)
 SHAPES = [(2, 20, 20, 64, 3), (1, 17, 33, 48, 5), (3, 40, 40, 32, 7), (2, 13, 9, 16, 9), (1, 80, 80, 64, 9),
           (2, 8, 70, 40, 5), (2, 24, 80, 32, 3), (2, 11, 45, 24, 7), (2, 40, 40, 128, 3), (1, 9, 23, 192, 3),
           (2, 16, 64, 64, 3), (1, 12, 96, 40, 7), (2, 20, 20, 128, 9),
           (2, 21, 30, 40, 9), (40, 20, 20, 256, 9), (2, 19, 70, 24, 5), (1, 33, 96, 40, 5),
-          (2, 18, 28, 48, 7), (16, 40, 40, 256, 7), (2, 17, 50, 24, 9), (2, 12, 24, 32, 5)]
+          (2, 18, 28, 48, 7), (16, 40, 40, 256, 7), (2, 17, 50, 24, 9), (2, 12, 24, 32, 5),
+          (2, 25, 16, 16, 5), (1, 32, 32, 24, 7)]
 TOL = {"f32": 2e-5, "bf16": 1e-2, "f16": 2e-3}
 # f16 through the 16-bit paths (the MFMA kernels' f16 builtins) on the k >= 5 shapes
 F16_SHAPES = [sh for sh in SHAPES if sh[4] >= 5]

@@ -762,12 +762,14 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
 // items are 4 pixels x 8 channels of one row: four 16-B raw-buffer loads (out-of-image pixels read
 // as zeros through the range check), re-paired per channel with v_perm into eight 8-B LDS writes;
 // the next unit's items are loaded into registers while the current one computes.
-template <int K, int NCH, int CG>
+template <int K, int NCH, int CG, int NB>
 struct DwWgM {
-  static constexpr int P = K / 2, PA = 4, SH = PA - P, XR = 16 + K - 1, NT = 32 * CG, NW = CG / 2, H2 = CG / 8;
+  // NB 16-row dz blocks per unit (2: a 20- or 32-row map is one unit, staged once)
+  static constexpr int P = K / 2, PA = 4, SH = PA - P, DR = 16 * NB, XR = DR + K - 1, NT = 32 * CG, NW = CG / 2;
+  static constexpr int H2 = CG / 8;
   static constexpr int XL = NCH == 1 ? 48 : (NCH == 2 ? 80 : 112);   // row stride (elements), both operands'
-  static constexpr int XE = CG * XR * XL, LDS_EL = XE + CG * 16 * XL;
-  static constexpr int NIX = (XR * 8 * NCH * H2 + NT - 1) / NT, NID = (16 * 8 * NCH * H2 + NT - 1) / NT;
+  static constexpr int XE = CG * XR * XL, LDS_EL = XE + CG * DR * XL;
+  static constexpr int NIX = (XR * 8 * NCH * H2 + NT - 1) / NT, NID = (DR * 8 * NCH * H2 + NT - 1) / NT;
   static_assert(XL >= 32 * NCH + 8, "row holds the chunks and the window overhang");
   static_assert(LDS_EL * 2 <= (CG == 8 ? 80 : 160) * 1024 && NW * 512 * 4 <= LDS_EL * 2, "LDS");
 };
@@ -787,12 +789,13 @@ __device__ __forceinline__ u32x4 dw_window(const unsigned (&v)[8], int s) {
   return u32x4{__builtin_amdgcn_alignbit(v[m + 1], v[m], 16), __builtin_amdgcn_alignbit(v[m + 2], v[m + 1], 16),
                __builtin_amdgcn_alignbit(v[m + 3], v[m + 2], 16), __builtin_amdgcn_alignbit(v[m + 4], v[m + 3], 16)};
 }
-template <typename T, int K, int NCH, int CG>
+template <typename T, int K, int NCH, int CG, int NB>
 __global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_kernel(DwParams p, const char* dz,
                                                                                    int dz_ld, int dz_off, float* ws,
                                                                                    int nj, int upb, int ncg, int ngrp) {
-  using G = DwWgM<K, NCH, CG>;
+  using G = DwWgM<K, NCH, CG, NB>;
   constexpr int P = G::P, PA = G::PA, SH = G::SH, XR = G::XR, XL = G::XL, NT = G::NT, NW = G::NW, H2 = G::H2;
+  constexpr int DR = G::DR;
   constexpr int NIX = G::NIX, NID = G::NID;
   __shared__ __attribute__((aligned(16))) unsigned short lds[G::LDS_EL];
   unsigned short* xs = lds;
@@ -825,8 +828,8 @@ __global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_ke
 #pragma unroll
   for (int i = 0; i < NID; ++i) {
     const int it = tid + NT * i, h = it % H2, rm = it / H2, r = rm / ng, m = rm - r * ng;
-    const bool ok = r < 16 && c0 + 8 * h < p.C;
-    dslot[i] = (8 * h * 16 + r) * XL + 4 * m;
+    const bool ok = r < DR && c0 + 8 * h < p.C;
+    dslot[i] = (8 * h * DR + r) * XL + 4 * m;
     doff[i] = ok ? (int)((((uint32_t)r * p.W + 4 * m) * dz_ld + 8 * h) * 2) : -1;
     dr_[i] = r;
     dm[i] = ok ? min(4, p.W - 4 * m) : 0;
@@ -843,7 +846,7 @@ __global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_ke
     const int n = unit / nj, j = unit - n * nj;
     const char* xi = xsrc + n * ximg;
     const char* di = dsrc + n * dimg;
-    const int yx = 16 * j - P, yd = 16 * j;   // image row of staged row 0
+    const int yx = DR * j - P, yd = DR * j;   // image row of staged row 0
 #pragma unroll
     for (int i = 0; i < NIX; ++i) {
       const int y = yx + xr_[i];
@@ -885,7 +888,7 @@ __global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_ke
       if (xoff[i] >= 0) put(xs + xslot[i], XR * XL, xv[i]);
 #pragma unroll
     for (int i = 0; i < NID; ++i)
-      if (doff[i] >= 0) put(ds + dslot[i], 16 * XL, dv[i]);
+      if (doff[i] >= 0) put(ds + dslot[i], DR * XL, dv[i]);
   };
   const int lane = tid & 63, w = tid >> 6, r16 = lane & 15, g = lane >> 4;
   f32x4 acc[2][2][K];   // [channel of the wave][diagonal / lower block][dx]
@@ -897,21 +900,27 @@ __global__ __launch_bounds__(32 * CG, CG == 8 ? 2 : 1) void dwconv_wgrad_mfma_ke
       for (int dx = 0; dx < K; ++dx) acc[cl][s][dx] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto compute = [&](int unit) {
     const int j = unit % nj;
-    const bool lower = 16 * j + 16 - P < p.H;   // the lower block's input rows are not all padding
 #pragma unroll
-    for (int cl = 0; cl < 2; ++cl) {
-      const int ch = w + NW * cl;
+    for (int jj = 0; jj < NB; ++jj) {
+      const int b0 = DR * j + 16 * jj;               // image row of this dz block's first row
+      if (b0 >= p.H) break;
+      const bool lower = b0 + 16 - P < p.H;          // the lower block's input rows are not all padding
 #pragma unroll
-      for (int q = 0; q < NCH; ++q) {
-        const u32x4 bw = *reinterpret_cast<const u32x4*>(ds + (ch * 16 + r16) * XL + 32 * q + 8 * g);
+      for (int cl = 0; cl < 2; ++cl) {
+        const int ch = w + NW * cl;
 #pragma unroll
-        for (int s = 0; s < 2; ++s) {
-          if (s == 1 && !lower) break;
-          const unsigned short* xr = xs + (ch * XR + 16 * s + r16) * XL + 32 * q + 8 * g;
-          const u32x4 v0 = *reinterpret_cast<const u32x4*>(xr), v1 = *reinterpret_cast<const u32x4*>(xr + 8);
-          const unsigned v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+        for (int q = 0; q < NCH; ++q) {
+          const u32x4 bw = *reinterpret_cast<const u32x4*>(ds + (ch * DR + 16 * jj + r16) * XL + 32 * q + 8 * g);
 #pragma unroll
-          for (int dx = 0; dx < K; ++dx) acc[cl][s][dx] = mfma16x16x32<T>(dw_window(v, dx + SH), bw, acc[cl][s][dx]);
+          for (int s = 0; s < 2; ++s) {
+            if (s == 1 && !lower) break;
+            const unsigned short* xr = xs + (ch * XR + 16 * (jj + s) + r16) * XL + 32 * q + 8 * g;
+            const u32x4 v0 = *reinterpret_cast<const u32x4*>(xr), v1 = *reinterpret_cast<const u32x4*>(xr + 8);
+            const unsigned v[8] = {v0[0], v0[1], v0[2], v0[3], v1[0], v1[1], v1[2], v1[3]};
+#pragma unroll
+            for (int dx = 0; dx < K; ++dx)
+              acc[cl][s][dx] = mfma16x16x32<T>(dw_window(v, dx + SH), bw, acc[cl][s][dx]);
+          }
         }
       }
     }
@@ -1376,16 +1385,21 @@ static bool dw_wgm(const yms_dw_shape* s) {
   return s->k >= 5 && s->dtype != YMS_F32 && (s->w <= 64 || (s->w <= 96 && s->k == 5));
 }
 struct DwWgmCfg {
-  int nch, nj, ncg, upb, groups;
+  int nch, nb, nj, ncg, upb, groups;
 };
-// units = (image, 16 dz rows); 16 channels per block (512 threads, one block per CU: 8 waves of
+#ifndef DW_WGM_NB2
+#define DW_WGM_NB2 1   // dev A/B switch (0: 16-row units only)
+#endif
+// units = (image, 16 dz rows; 32 for maps of 17-32 rows and one column chunk); 16 channels per block (512 threads, one block per CU: 8 waves of
 // ~220 VGPRs; 32-B pixel pieces per block, measured 4-8 % faster on k = 7 than 8-channel blocks at
 // two per CU, equal on k = 9); units per block: the fewest that keep the grid within one round of
 // the resident blocks; each unit group adds one ws row per tap and channel
 static DwWgmCfg dw_wgm_cfg(const yms_dw_shape* s) {
   DwWgmCfg c;
   c.nch = (s->w + 31) / 32;
-  c.nj = (s->h + 15) / 16;
+  // maps of 17-32 rows and one column chunk: both 16-row dz blocks in one unit (one staging)
+  c.nb = DW_WGM_NB2 && c.nch == 1 && s->h > 16 && s->h <= 32 ? 2 : 1;
+  c.nj = (s->h + 16 * c.nb - 1) / (16 * c.nb);
   c.ncg = (s->c + DW_WGM_CG - 1) / DW_WGM_CG;
   const long units = (long)s->n * c.nj, slots = (DW_WGM_CG == 8 ? 2l : 1l) * conv_cu_count();
   c.upb = (int)std::max(1l, (units * c.ncg + slots - 1) / slots);
@@ -1594,21 +1608,24 @@ yms_status yms_dwconv_wgrad(const yms_dw_shape* s, const void* x, int x_ld, int 
     const DwWgmCfg c = dw_wgm_cfg(s);
     blocks = c.groups;
     const dim3 grid((unsigned)(((long)c.groups * c.ncg + 7) / 8 * 8));
-#define YMS_DWM_L(KV, NV)                                                                                   \
-  hipLaunchKernelGGL((dwconv_wgrad_mfma_kernel<TT, KV, NV, DW_WGM_CG>), grid, dim3(32 * DW_WGM_CG), 0, st, p,          \
-                     (const char*)dz, dz_ld, dz_off, \
-                     ws, c.nj, c.upb, c.ncg, c.groups)
+#define YMS_DWM_L(KV, NV, NBV)                                                                              \
+  hipLaunchKernelGGL((dwconv_wgrad_mfma_kernel<TT, KV, NV, DW_WGM_CG, NBV>), grid, dim3(32 * DW_WGM_CG), 0, st, p,     \
+                     (const char*)dz, dz_ld, dz_off, ws, c.nj, c.upb, c.ncg, c.groups)
     YMS_DW_T16(s->dtype, {
-      if (c.nch == 1) {
-        if (s->k == 5) YMS_DWM_L(5, 1);
-        else if (s->k == 7) YMS_DWM_L(7, 1);
-        else YMS_DWM_L(9, 1);
+      if (c.nch == 1 && c.nb == 2) {
+        if (s->k == 5) YMS_DWM_L(5, 1, 2);
+        else if (s->k == 7) YMS_DWM_L(7, 1, 2);
+        else YMS_DWM_L(9, 1, 2);
+      } else if (c.nch == 1) {
+        if (s->k == 5) YMS_DWM_L(5, 1, 1);
+        else if (s->k == 7) YMS_DWM_L(7, 1, 1);
+        else YMS_DWM_L(9, 1, 1);
       } else if (c.nch == 2) {
-        if (s->k == 5) YMS_DWM_L(5, 2);
-        else if (s->k == 7) YMS_DWM_L(7, 2);
-        else YMS_DWM_L(9, 2);
+        if (s->k == 5) YMS_DWM_L(5, 2, 1);
+        else if (s->k == 7) YMS_DWM_L(7, 2, 1);
+        else YMS_DWM_L(9, 2, 1);
       } else {
-        YMS_DWM_L(5, 3);
+        YMS_DWM_L(5, 3, 1);
       }
     });
 #undef YMS_DWM_L
