@@ -17,7 +17,7 @@ pytestmark = pytest.mark.gpu
 # the tile width follows the map width (32 where it divides it, else 40 / 20 / 32: every width below
 # is covered), and k = 3 with C % 64 == 0 takes 64-channel blocks: the list holds each kernel
 # geometry -- TX 20 (w 20, 9), 40 (33, 40, 80, 23), 32 (70, 45, 64, 96), 64-channel k = 3 blocks
-# (C 64 / 128 / 192), 32-channel blocks for every k; fp32 runs the tile weight-gradient kernel.
+# (C 64 / 128 / 192), 56-channel k = 3 blocks (C 112 / 168), 32-channel blocks for every k; fp32 runs the tile weight-gradient kernel.
 # 16-bit k = 5 / 7 / 9 at widths <= 64 (k = 5: 96) take the MFMA weight gradient: one (w 9, 20, 24,
 # 28, 30), two (33, 40, 45, 50) and three (70, 96) column chunks (each k with one and two), partial
 # channel groups (C 24, 40), partial last row blocks (h 13, 19, 21, 33), several units per block
@@ -29,7 +29,7 @@ SHAPES = [(2, 20, 20, 64, 3), (1, 17, 33, 48, 5), (3, 40, 40, 32, 7), (2, 13, 9,
           (2, 16, 64, 64, 3), (1, 12, 96, 40, 7), (2, 20, 20, 128, 9),
           (2, 21, 30, 40, 9), (40, 20, 20, 256, 9), (2, 19, 70, 24, 5), (1, 33, 96, 40, 5),
           (2, 18, 28, 48, 7), (16, 40, 40, 256, 7), (2, 17, 50, 24, 9), (2, 12, 24, 32, 5),
-          (2, 25, 16, 16, 5), (1, 32, 32, 24, 7)]
+          (2, 25, 16, 16, 5), (1, 32, 32, 24, 7), (2, 24, 40, 112, 3), (1, 20, 20, 168, 3)]
 TOL = {"f32": 2e-5, "bf16": 1e-2, "f16": 2e-3}
 # f16 through the 16-bit paths (the MFMA kernels' f16 builtins) on the k >= 5 shapes
 F16_SHAPES = [sh for sh in SHAPES if sh[4] >= 5]

@@ -163,7 +163,7 @@ __device__ __forceinline__ Raw8<T> pack_raw8(const float (&v)[8]) {
 }
 
 template <typename T, int K, int MODE, int TX = DW_TX, int G = DW_G>
-__global__ __launch_bounds__(G * 64, (G == 8 ? 2 : DwOcc<T, K>::v))
+__global__ __launch_bounds__(G * 64, (G >= 7 ? 2 : DwOcc<T, K>::v))
 void dwconv_kernel(DwParams p) {
   constexpr int CB = G * 8, NT = G * 64;
   constexpr int TY = DwTy<TX>::v, CGX = TX / DW_RX;
@@ -1273,13 +1273,18 @@ static int dw_occ(const yms_dw_shape* s) {
 }
 
 // channel groups of 8 per forward / dgrad block: 8 (64 channels = one 128-B line of an NHWC pixel
-// per block, 512 threads) for k = 3 when C is a multiple of 64, else 4 (32 channels: the other half
-// of each line is read and written by another block at another time).
-#ifndef DW_G8_ANY
-#define DW_G8_ANY 0
+// per block, 512 threads) for k = 3 when C is a multiple of 64, 7 (56 channels) for k = 3 when C is a
+// multiple of 56 but not of 32, else 4 (32 channels: the other part of each line is read and written
+// by the neighbouring blocks, on the same XCD).
+#ifndef DW_G7
+#define DW_G7 1   // dev A/B switch (0: 32-channel blocks)
 #endif
 static int dw_fwd_g(const yms_dw_shape* s) {
-  return s->k == 3 && (s->c % 64 == 0 || (DW_G8_ANY && s->c > 64)) && s->dtype != YMS_F32 ? 8 : 4;
+  if (s->k != 3 || s->dtype == YMS_F32) return 4;
+  if (s->c % 64 == 0) return 8;
+  // 56-channel blocks (448 threads) where 32-channel blocks would leave lanes idle: C = 112, 168, ...
+  // (k3@160 c112 fwd 306 -> 282 us, dgrad 289 -> 253 us; profiles/r05ze_dw_g7_ab.txt)
+  return DW_G7 && s->c % 32 != 0 && s->c % 56 == 0 ? 7 : 4;
 }
 
 // forward / dgrad grid: image column tiles split into strips of tps tiles.  The strip length is
@@ -1291,7 +1296,7 @@ static dim3 dw_strip_grid(const yms_dw_shape* s, DwParams& p) {
   const int TY = dw_fwd_ty(dw_fwd_tx(s)), G = dw_fwd_g(s);
   const long cg = (s->c + 8 * G - 1) / (8 * G);
   const long base = (long)s->n * p.tiles_x * cg;
-  const long slots = (long)(G == 8 ? 2 : dw_occ(s)) * conv_cu_count();
+  const long slots = (long)(G >= 7 ? 2 : dw_occ(s)) * conv_cu_count();
   double best = 1e30;
   int best_tps = p.tiles_y;
   for (int tps = p.tiles_y; tps >= 1; --tps) {
@@ -1535,6 +1540,13 @@ yms_status yms_dwconv_fwd(const yms_dw_shape* s, const void* x, int x_ld, int x_
     }));
     return launch_status();
   }
+  if (dw_fwd_g(s) == 7) {
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, {
+      if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_STATS, TXX, 7>), grid, dim3(448), 0, st, p);
+      else hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_FWD_AFFINE, TXX, 7>), grid, dim3(448), 0, st, p);
+    }));
+    return launch_status();
+  }
   YMS_DW_T(s->dtype, YMS_DW_K(s->k, YMS_DW_TXS(TX, {
     if (stats) hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_STATS, TXX>), grid, dim3(256), 0, st, p);
     else hipLaunchKernelGGL((dwconv_kernel<TT, KK, DW_FWD_AFFINE, TXX>), grid, dim3(256), 0, st, p);
@@ -1563,6 +1575,11 @@ yms_status yms_dwconv_dgrad(const yms_dw_shape* s, const void* dz, int dz_ld, in
   const int TX = dw_fwd_tx(s);
   if (dw_fwd_g(s) == 8) {
     YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_DGRAD, TXX, 8>), grid, dim3(512), 0,
+                                                           st, p)));
+    return launch_status();
+  }
+  if (dw_fwd_g(s) == 7) {
+    YMS_DW_T16(s->dtype, YMS_DW_TXS(TX, hipLaunchKernelGGL((dwconv_kernel<TT, 3, DW_DGRAD, TXX, 7>), grid, dim3(448), 0,
                                                            st, p)));
     return launch_status();
   }
