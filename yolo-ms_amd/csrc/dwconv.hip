@@ -756,12 +756,14 @@ __global__ __launch_bounds__(G * 64, 2) void dwconv_wgrad3_kernel(DwParams p, co
 // chunk and reused by 2 K products; the input fragment (lane: row a, 16 columns) once per block and
 // chunk, the K column windows dx = 0 .. K-1 cut from registers (dword selects / v_alignbit).  At the
 // end each wave sums the 16 entries of every diagonal through LDS in a fixed order and writes
-// ws[group][t][c]; a reduce kernel sums the groups.  LDS holds a unit channel-major (8 channels:
-// 16 + K - 1 input rows, 16 dz rows; image column x of the input at x + 4), rows 96 / 160 B apart: the
-// 16 rows one ds_read_b128 lane group touches (two column slots) fall in distinct banks.  Staging
-// items are 4 pixels x 8 channels of one row: four 16-B raw-buffer loads (out-of-image pixels read
-// as zeros through the range check), re-paired per channel with v_perm into eight 8-B LDS writes;
-// the next unit's items are loaded into registers while the current one computes.
+// ws[group][t][c]; a reduce kernel sums the groups.  A block is 16 channels (512 threads, two
+// channels per wave; neighbouring lanes load the two 16-B halves of a pixel's 32 B).  LDS holds a unit
+// channel-major (16 NB + K - 1 input rows, 16 NB dz rows; image column x of the input at x + 4), rows
+// 96 / 160 / 224 B apart: the 16 rows one ds_read_b128 lane group touches (two column slots) fall in
+// distinct banks.  NB = 2 for maps of 17-32 rows (one staging for both dz blocks).  Staging items
+// are 4 pixels x 8 channels of one row: four 16-B loads (rows outside the image load as zeros,
+// columns past the map are never loaded), re-paired per channel with v_perm into eight 8-B LDS
+// writes; the next unit's items are loaded into registers while the current one computes.
 template <int K, int NCH, int CG, int NB>
 struct DwWgM {
   // NB 16-row dz blocks per unit (2: a 20- or 32-row map is one unit, staged once)
