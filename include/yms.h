@@ -89,6 +89,11 @@ yms_status yms_conv_pack_weights_batched(int njobs, const yms_pack_job* jobs_dev
  * rows * (2*stats_ld + 1) floats), stats_ld = yms_conv_stats_ld(). */
 int yms_conv_stats_rows(const yms_conv_shape* s);
 int yms_conv_stats_ld(const yms_conv_shape* s);
+/* Process-wide route switch of the direct small-channel 3x3 kernel (conv_direct.hip; default on,
+ * YMS_DIRECT=0 in the environment at the first call turns it off).  on = 0 / 1 sets it, on < 0 only
+ * queries; returns the previous setting.  It changes yms_conv_stats_rows, so callers flip it only
+ * while no plan sized under the other setting is in use (tests and A/B runs). */
+int yms_conv_direct_set(int on);
 /* Forward.  stats == NULL: y = act(conv(x)*scale[c] + shift[c]) (+ res) (scale/shift may
  * be NULL = identity).  stats != NULL (training): y = conv(x) (pre-BN z) and statistics rows
  * (sum z, sum (z - row mean)^2, pixel count) into stats. */
@@ -96,17 +101,6 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
                         const void* wpacked, void* y, int y_ld, int y_off,
                         const float* scale, const float* shift, int act,
                         const void* res, int res_ld, int res_off, float* stats, void* stream);
-/* Training forward whose input is the PRODUCER's pre-BN output z (components.py:72-74 of the conv
- * before this one): x = act(z*in_scale[c] + in_shift[c]) is formed from each staged input tile
- * (act: YMS_ACT_NONE / YMS_ACT_SILU, the producer's yms_affine_act formula and rounding) and,
- * from the centre tap of the first output-column tile, also written to x (x_ld, x_off): the
- * producer's separate affine pass (read z, write x) is replaced by this write.  Otherwise as
- * yms_conv_fwd with stats != NULL (y = conv(x), statistics rows).  Supported:
- * yms_conv_fwd_pro_supported(s): 16-bit, stride 1, pad k/2 ("same"), cin % 8 == 0, cin <= 1024. */
-int yms_conv_fwd_pro_supported(const yms_conv_shape* s);
-yms_status yms_conv_fwd_pro(const yms_conv_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
-                            const float* in_shift, int in_act, void* x, int x_ld, int x_off, const void* wpacked,
-                            void* y, int y_ld, int y_off, float* stats, void* stream);
 /* Stem convolution (yolov8_backbone.py:30-40, the backbone's first Conv(cin, c1, 3, 2, 1), replacing
  * the NHWC input pack + yms_conv_fwd pair): x is the model's NCHW fp32 input [n][cin][h][w], w the
  * fp32 nn.Conv2d weight [cout][cin][3][3] (rounded to s->dtype in the kernel, as the packing

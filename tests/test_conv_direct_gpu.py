@@ -2,7 +2,7 @@
 yms_conv_fwd / yms_conv_dgrad take for 16-bit 3x3 stride-1 convs with 32 / 64 reduction channels
 and <= 64 output channels (components.py:69-93 Bottleneck convs of the 160^2 / 80^2 C2f stages, the
 80^2 head branches) -- against fp32 PyTorch on the same dtype-rounded operands, and against the
-implicit-GEMM path of the same op (YMS_DIRECT=0).  Covers both tile widths (TW 32 / 16), both
+implicit-GEMM path of the same op (yms_conv_direct_set(0)).  Covers both tile widths (TW 32 / 16), both
 reduction widths, one and two output fragments, ragged map heights, padded input channels, channel
 slices of wider buffers, every epilogue (BN+SiLU+residual, statistics, store, accumulate)."""
 import ctypes
@@ -42,16 +42,25 @@ def _direct_rows(sh):
     return L.lib().yms_conv_stats_rows(ctypes.pointer(sh))
 
 
-def test_direct_route_taken(monkeypatch):
-    """The direct kernel's statistics rows are one per persistent block (<= ntiles); YMS_DIRECT=0
-    restores the NT kernels' row count (one per block and 128-row half of its tiles)."""
+@pytest.fixture
+def direct_switch():
+    """yms_conv_direct_set(on) for the test, the process' setting restored after it."""
+    prev = L.lib().yms_conv_direct_set(-1)
+    yield lambda on: L.lib().yms_conv_direct_set(int(on))
+    L.lib().yms_conv_direct_set(prev)
+
+
+def test_direct_route_taken(direct_switch):
+    """The direct kernel's statistics rows are one per persistent block (<= ntiles); the route
+    switched off (yms_conv_direct_set(0), YMS_DIRECT=0 at start-up) restores the NT kernels' row
+    count (one per block and 128-row half of its tiles)."""
     sh = shape(64, 80, 80, 64, 64, 3, 1, torch.bfloat16)
     ntiles = 64 * (80 // 16) * (80 // 16)
     rows = _direct_rows(sh)
     assert 1 <= rows <= ntiles
-    monkeypatch.setenv("YMS_DIRECT", "0")
+    direct_switch(0)
     assert _direct_rows(sh) != rows
-    monkeypatch.delenv("YMS_DIRECT")
+    direct_switch(1)
     assert _direct_rows(shape(64, 80, 80, 128, 64, 3, 1, torch.bfloat16)) != rows   # 128-ch reduction: NT
 
 
@@ -142,9 +151,9 @@ def test_direct_channel_slices():
 
 
 @pytest.mark.parametrize("shp", [(64, 64, 80, 80, 64), (64, 32, 160, 160, 32), (8, 32, 320, 320, 32)])
-def test_direct_matches_implicit_gemm_bench_shapes(shp, monkeypatch):
+def test_direct_matches_implicit_gemm_bench_shapes(shp, direct_switch):
     """Bench-scale layers (B=64 S@640 stages; the S@1280 320^2 stage): forward with statistics and
-    input gradient of the direct kernel against the implicit-GEMM kernels (YMS_DIRECT=0) on the same
+    input gradient of the direct kernel against the implicit-GEMM kernels (route off) on the same
     operands -- both fp32-accumulated MFMA sums of the same products, so they agree to the bf16
     rounding of the output."""
     n, cin, h, w, cout = shp
@@ -158,7 +167,7 @@ def test_direct_matches_implicit_gemm_bench_shapes(shp, monkeypatch):
     wp, wpt = pack(wt, sh, dtype, 0), pack(wt, sh, dtype, 1)
     outs = {}
     for mode in ("1", "0"):
-        monkeypatch.setenv("YMS_DIRECT", mode)
+        direct_switch(int(mode))
         rows, ld = L.lib().yms_conv_stats_rows(sp), L.lib().yms_conv_stats_ld(sp)
         stt = torch.full((rows * (2 * ld + 1),), float("nan"), device="cuda")
         y = torch.empty(n, h, w, cout, dtype=dtype, device="cuda")
@@ -218,9 +227,9 @@ def test_direct_dgrad_stride2(shp, dt):
         assert dx[..., r8(cin):].abs().max().item() == 0
 
 
-def test_direct_dgrad_stride2_bench_shape(monkeypatch):
+def test_direct_dgrad_stride2_bench_shape(direct_switch):
     """The 320^2 32->64 stride-2 layer of the S@640 backbone: direct kernel vs the implicit GEMM's
-    parity-class path (YMS_DIRECT=0) on the same operands."""
+    parity-class path (route off) on the same operands."""
     n, cin, h, w, cout = 16, 32, 320, 320, 64
     dtype = torch.bfloat16
     g = torch.Generator(device="cuda").manual_seed(6)
@@ -231,7 +240,7 @@ def test_direct_dgrad_stride2_bench_shape(monkeypatch):
     wpt = pack(wt, sh, dtype, 1)
     outs = []
     for mode in ("1", "0"):
-        monkeypatch.setenv("YMS_DIRECT", mode)
+        direct_switch(int(mode))
         dx = torch.empty(n, h, w, cin, dtype=dtype, device="cuda")
         L.call("yms_conv_dgrad", sp, dz.data_ptr(), cout, 0, wpt.data_ptr(), dx.data_ptr(), cin, 0, 0,
                L.stream_ptr())

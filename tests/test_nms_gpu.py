@@ -99,6 +99,45 @@ def test_single_class_large_segment():
     _check(pred, 0.25, 0.5)
 
 
+def test_min_workspace_same_keep_lists():
+    """A caller holding only yms_nms_ws_bytes_min bytes on segments of >= YMS_NMS_GRAPH_MIN boxes
+    (sparse overlaps: the graph route's regime) gets the other exact routes: the keep lists and
+    counts equal those of a call with the full yms_nms_ws_bytes workspace, and the oracle's."""
+    import ctypes
+    from yms import _lib as L
+    rng = np.random.default_rng(21)
+    B, A, nc = 2, 8400, 1
+    pred = np.zeros((B, A, 4 + nc), np.float32)
+    pred[..., :2] = rng.uniform(0, 640, (B, A, 2))
+    pred[..., 2:4] = rng.uniform(4, 24, (B, A, 2))
+    pred[..., 4] = rng.uniform(0.3, 1.0, (B, A))
+    d = torch.from_numpy(pred).cuda()
+    st = L.stream_ptr(d.device)
+    bxy = torch.empty((B, A, 4), dtype=torch.float32, device="cuda")
+    score = torch.empty((B, A), dtype=torch.float32, device="cuda")
+    label = torch.empty((B, A), dtype=torch.int32, device="cuda")
+    L.call("yms_nms_prep", B, A, nc, d.data_ptr(), ctypes.c_float(0.25), bxy.data_ptr(), score.data_ptr(),
+           label.data_ptr(), st)
+    outs = []
+    for fn in (L.lib().yms_nms_ws_bytes, L.lib().yms_nms_ws_bytes_min):
+        nb = fn(B, A, nc)
+        ws = torch.empty(nb, dtype=torch.uint8, device="cuda")
+        keep = torch.full((B, A), -7, dtype=torch.int64, device="cuda")
+        klbl = torch.empty((B, A), dtype=torch.int32, device="cuda")
+        cnt = torch.empty(B, dtype=torch.int32, device="cuda")
+        L.call("yms_nms_classwise", B, A, nc, bxy.data_ptr(), score.data_ptr(), label.data_ptr(),
+               ctypes.c_double(0.5), keep.data_ptr(), klbl.data_ptr(), cnt.data_ptr(), ws.data_ptr(), nb, st)
+        c = cnt.cpu().numpy()
+        outs.append((c, [keep[b, :c[b]].cpu().numpy() for b in range(B)]))
+    assert L.lib().yms_nms_ws_bytes_min(B, A, nc) < L.lib().yms_nms_ws_bytes(B, A, nc)
+    (c_full, k_full), (c_min, k_min) = outs
+    assert np.array_equal(c_full, c_min)
+    for b in range(B):
+        assert np.array_equal(k_full[b], k_min[b])
+        ki = onms.postprocess(pred[b], 0.25, 0.5)[0]
+        assert np.array_equal(k_min[b], ki)
+
+
 def test_ties_and_duplicates():
     """Exact score ties keep anchor order; identical boxes suppress; empty classes skipped."""
     A, nc = 64, 3

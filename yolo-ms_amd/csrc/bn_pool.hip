@@ -248,15 +248,9 @@ __device__ __forceinline__ void load_params8(const float* p, int c0, int c, floa
 // U pixels per thread per iteration: all U loads issue before any use (memory-level
 // parallelism; these kernels are HBM-bound).
 constexpr int BN_U = 4;
-// the backward reduce / apply passes (dev A/B builds; at 8 the YOLOv8-s step went 17.80 -> 17.90 ms
+// the backward reduce / apply passes (8 measured slower: the YOLOv8-s step went 17.80 -> 17.90 ms
 // (reduce) and -> 19.43 ms (apply), profiles/r05u_bn_unroll_ab.txt)
-#ifndef YMS_BN_UR
-#define YMS_BN_UR 4
-#endif
-#ifndef YMS_BN_UA
-#define YMS_BN_UA 4
-#endif
-constexpr int BN_UR = YMS_BN_UR, BN_UA = YMS_BN_UA;
+constexpr int BN_UR = 4, BN_UA = 4;
 
 // Pixel-range order of the elementwise passes over a tensor: blocks are dispatched in index order,
 // so block b taking range nblocks - 1 - b walks the tensor from its end.  A pass that follows one
@@ -264,16 +258,8 @@ constexpr int BN_UR = YMS_BN_UR, BN_UA = YMS_BN_UA;
 // ones still held by the 256 MB memory-side cache -- instead of the ones it evicted first.
 // Interleaved A/B (YOLOv8-s B=64 step, 3 reps, profiles/r05r_bn_order_ab.txt): the forward affine
 // pass reversed (after the conv that wrote z) 18.22 -> 18.17 ms; also reversing the backward
-// reduce or apply gave no more.  Compile-time switches for dev A/B builds (tools/ab_lib.sh).
-#ifndef YMS_REV_AFFINE
-#define YMS_REV_AFFINE 1
-#endif
-#ifndef YMS_REV_RED
-#define YMS_REV_RED 0
-#endif
-#ifndef YMS_REV_APPLY
-#define YMS_REV_APPLY 0
-#endif
+// reduce or apply gave no more.
+constexpr bool BN_REV_AFFINE = true, BN_REV_RED = false, BN_REV_APPLY = false;
 template <bool REV> __device__ __forceinline__ long block_range() {
   return REV ? (long)(gridDim.x - 1 - blockIdx.x) : (long)blockIdx.x;
 }
@@ -291,7 +277,7 @@ __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const
   float sc[8], sh[8];
   load_params8(scale, c0, c, sc, 1.0f);
   load_params8(shift, c0, c, sh, 0.0f);
-  const long p0 = block_range<YMS_REV_AFFINE>() * ppb, p1 = min(npix, p0 + ppb);
+  const long p0 = block_range<BN_REV_AFFINE>() * ppb, p1 = min(npix, p0 + ppb);
   auto emit = [&](long pix, const Raw8<T>& zz, const Raw8<T>& rres, int valid) {
     float v[8], r[8];
     unpack8(zz, v);
@@ -388,7 +374,7 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
       load_params8(mi, c0, c, mu, 0.f);
       load_params8(mi + c, c0, c, is, 0.f);
     }
-    const long p0 = block_range<YMS_REV_RED>() * ppb, p1 = min(npix, p0 + ppb);
+    const long p0 = block_range<BN_REV_RED>() * ppb, p1 = min(npix, p0 + ppb);
     auto accum = [&](const Raw8<T>& g, const Raw8<T>& zz) {
       float gv[8], zv[8];
       unpack8(g, gv);
@@ -472,11 +458,11 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
       float t1 = 0.f, t2 = 0.f;
       for (int l = 0; l < lanes; ++l) { t1 += red[0][l * W + ch]; t2 += red[1][l * W + ch]; }
       if (lane0 == 0) {
-        ws[block_range<YMS_REV_RED>() * 2 * c + ch] = t1;          // row = the block's pixel range
-        ws[block_range<YMS_REV_RED>() * 2 * c + c + ch] = t2;
+        ws[block_range<BN_REV_RED>() * 2 * c + ch] = t1;          // row = the block's pixel range
+        ws[block_range<BN_REV_RED>() * 2 * c + c + ch] = t2;
       } else {
-        ws[block_range<YMS_REV_RED>() * 2 * c + ch] += t1;
-        ws[block_range<YMS_REV_RED>() * 2 * c + c + ch] += t2;
+        ws[block_range<BN_REV_RED>() * 2 * c + ch] += t1;
+        ws[block_range<BN_REV_RED>() * 2 * c + c + ch] += t2;
       }
     }
     __syncthreads();
@@ -610,7 +596,7 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
       A[i] = -sc[i] * k0[i] - Bz[i] * mu[i];
     }
   }
-  const long p0 = block_range<YMS_REV_APPLY>() * ppb, p1 = min(npix, p0 + ppb);
+  const long p0 = block_range<BN_REV_APPLY>() * ppb, p1 = min(npix, p0 + ppb);
   const bool racc = gres && gres_acc;
   auto emit = [&](long pix, const Raw8<T>& g, const Raw8<T>& zz, const Raw8<T>& rres, int valid) {
     float gv[8], zv[8], out[8];

@@ -31,11 +31,6 @@
 #include "conv_common.hpp"
 #include "conv_direct.hpp"
 
-// dev-only diagnostic builds (tools/ab_lib.sh "-DYMS_DIRECT_DIAG=n"): 1 no per-tile statistics
-// update, 3 no MFMAs, 4 no output stores, 5 no halo loads, 6 no MFMA operand reads after the first
-#ifndef YMS_DIRECT_DIAG
-#define YMS_DIRECT_DIAG 0
-#endif
 
 namespace yms {
 
@@ -201,7 +196,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
       const uint32_t vo =
           ok ? (uint32_t)(((pix0 + hl_hy[j] * p.W + hl_hx[j]) * p.src_ld + p.src_off) * ES + hl_c[j]) : NT_OOB;
       if (G::HGR % NTHR == 0 || j + 1 < G::NP || j * NTHR + tid < G::HGR)
-        if (YMS_DIRECT_DIAG != 5) blds16(rs_src, base + j * NTHR * 16, vo);
+        blds16(rs_src, base + j * NTHR * 16, vo);
     }
   };
 
@@ -285,13 +280,13 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
       // scheduling fences: the compiler would otherwise sink each read next to its MFMA (and wait
       // out the LDS latency there)
       __builtin_amdgcn_sched_barrier(0);
-      if (grp + 1 < NG && YMS_DIRECT_DIAG != 6) frags(grp + 1, (grp + 1) & 1);
+      if (grp + 1 < NG) frags(grp + 1, (grp + 1) & 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int j = 0; j < KG; ++j)
 #pragma unroll
         for (int cf = 0; cf < NCF; ++cf)
-          if constexpr (YMS_DIRECT_DIAG != 3) acc[cf] = Mfma<T>::mma(bf[grp & 1][j][cf], af[grp & 1][j], acc[cf]);
+          acc[cf] = Mfma<T>::mma(bf[grp & 1][j][cf], af[grp & 1][j], acc[cf]);
     }
     __builtin_amdgcn_sched_barrier(0);
   };
@@ -301,7 +296,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
     int n, tyi, txi;
     tile_pos(t, n, tyi, txi);
     const bool pix_ok = tyi * TH + oty < p.H;
-    if constexpr (EPI == EPI_STATS && YMS_DIRECT_DIAG != 1) {
+    if constexpr (EPI == EPI_STATS) {
       if (pix_ok) {
         wn += 1.f;
         const float inv = 1.0f / wn;
@@ -355,7 +350,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
         }
         bool ok;
         const uint32_t off = out_off(n, tyi, txi, cf, pp, p.dst_ld, p.dst_off, ok);
-        if constexpr (YMS_DIRECT_DIAG != 4) cd_st16(rs_dst, ok ? off : NT_OOB, ov);
+        cd_st16(rs_dst, ok ? off : NT_OOB, ov);
       }
     }
   };
@@ -540,7 +535,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
       const uint32_t vo =
           ok ? (uint32_t)(((pix0 + hl_hy[j] * p.W + hl_hx[j]) * p.src_ld + p.src_off) * ES + hl_c[j]) : NT_OOB;
       if (G::HGR % NTHR == 0 || j + 1 < G::NP || j * NTHR + tid < G::HGR)
-        if (YMS_DIRECT_DIAG != 5) blds16(rs_src, base + j * NTHR * 16, vo);
+        blds16(rs_src, base + j * NTHR * 16, vo);
     }
   };
   const int hr = wave * 32 + lr;
@@ -689,9 +684,19 @@ static int direct_occ(int tw, int cp, int ncf) {
   return ncf == 2 ? GEO<16, 4, 2>::OCC : GEO<16, 4, 1>::OCC;   // (constants only: nothing launched)
 }
 
+// Route switch, read ONCE per process from YMS_DIRECT (0 = off) and changed only through
+// yms_conv_direct_set: the route decides how many statistics rows a forward writes
+// (yms_conv_stats_rows), which a plan sizes when it is built, so it must not flip under a plan.
+static int& direct_route() {
+  static int on = [] {
+    const char* e = getenv("YMS_DIRECT");
+    return (e && atoi(e) == 0) ? 0 : 1;
+  }();
+  return on;
+}
+
 bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g) {
-  const char* e = getenv("YMS_DIRECT");
-  if (e && atoi(e) == 0) return false;
+  if (!direct_route()) return false;
   if (!s || s->dtype == YMS_F32 || s->k != 3 || s->pad != 1) return false;
   const bool s2 = s->stride == 2;
   if (s2 ? (mode != 1 || s->ho != (s->h + 1) / 2 || s->wo != (s->w + 1) / 2)
@@ -849,3 +854,9 @@ yms_status conv_direct_launch(const yms_conv_shape* s, int mode, const DirectGeo
 }
 
 }  // namespace yms
+
+extern "C" int yms_conv_direct_set(int on) {
+  const int prev = yms::direct_route();
+  if (on >= 0) yms::direct_route() = on ? 1 : 0;
+  return prev;
+}

@@ -19,7 +19,7 @@ struct DirectGeo {
 // 8 of 32 or 64, at most 64 output channels (a multiple of 8), map width a multiple of 16.
 // mode 0 = stride-1 forward (reduction = cin), 1 = input gradient (reduction = cout) of a stride-1
 // conv, or of a stride-2 conv by output parity class (grid width ceil(w / 2) a multiple of 16).
-// YMS_DIRECT=0 turns it off (A/B and tests; read per call).
+// Off when YMS_DIRECT=0 at the first call or after yms_conv_direct_set(0) (A/B and tests).
 bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g);
 
 yms_status conv_direct_launch(const yms_conv_shape* s, int mode, const DirectGeo& g, const void* src, int src_ld,

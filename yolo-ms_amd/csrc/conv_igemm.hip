@@ -55,15 +55,6 @@ struct NTParams {
   int cls_M[4], cls_nkt[4], cls_Kc[4], cls_ntx[4], cls_c0y[4], cls_c0x[4];
   long cls_woff[4];                 // byte offset of the class' packed weight block
   FastDiv cls_div_w[4], cls_div_hw[4];
-  // PRO (training forward, stride 1): src is the PRODUCER's pre-BN z; each A chunk is turned into
-  // x = act(z * pro_sc[c] + pro_sh[c]) in LDS before the MFMAs, and the centre-tap chunks of the
-  // first column tile are also stored to x (pro_x, pro_x_ld, pro_x_off): the producer's affine pass
-  // (read z, write x) becomes one write, and the conv reads z instead of x.
-  const float* pro_sc;
-  const float* pro_sh;
-  int pro_act;
-  char* pro_x;
-  int pro_x_ld, pro_x_off, pro_c;
 };
 
 // 16-B zero chunk: out-of-image / out-of-K im2col lanes load from here, so the A loads are
@@ -424,9 +415,7 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
 // 16-B row segments (+ residual / + accumulate in fp32).
 // ------------------------------------------------------------------------------------------
 constexpr int NTP_MAX_AFFINE_COLS = 512;   // wider affine outputs use conv_nt_kernel
-constexpr int NTP_PRO_MAX_C = 1024;        // input channels of a prologue (PRO) conv
-template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI, int OCC = 2,
-          bool PRO = false>
+template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI, int OCC = 2>
 __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams p) {
   constexpr int NTHR = WGM * WGN * 64;
   constexpr int RPP = NTHR / NT_KCH;                       // rows per load pass (one slot)
@@ -441,8 +430,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
   // [3][SROWS*BN] (kept in LDS: three more live VGPRs would cost a block per CU)
   constexpr int RED = (EPI == EPI_STATS) ? (WGM * 2 + 3 * (BM / 128 > 0 ? BM / 128 : 1)) * BN * 4 : 0;
   constexpr int PRM = (EPI == EPI_AFFINE) ? 2 * NTP_MAX_AFFINE_COLS * 4 : 0;
-  constexpr int PPR = PRO ? 2 * NTP_PRO_MAX_C * 4 : 0;
-  static_assert(!PRO || (MODE == MODE_FWD && sizeof(T) == 2), "prologue: 16-bit forward only");
   static_assert((B_PART || BN % RPP == 0) && BM % RPP == 0 && BN <= NTHR, "tile");
   // the output tile is staged through the ring stage just consumed, in NH passes of HR rows
   constexpr int NH = (BM * BN * (int)sizeof(T) > STAGE) ? 2 : 1;
@@ -454,10 +441,9 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
   // (yms_conv_stats_rows = SROWS x grid / tiles_n, counts after the rows)
   constexpr int SROWS = BM / 128 > 0 ? BM / 128 : 1;
   static_assert(BM % 128 == 0 && WGM % SROWS == 0, "statistics rows");
-  __shared__ __attribute__((aligned(16))) char smem[ST * STAGE + RED + PRM + PPR + 16];
+  __shared__ __attribute__((aligned(16))) char smem[ST * STAGE + RED + PRM + 16];
   float* red = reinterpret_cast<float*>(smem + ST * STAGE);
   float* prm = reinterpret_cast<float*>(smem + ST * STAGE + RED);   // [scale | shift] per column
-  float* ppr = reinterpret_cast<float*>(smem + ST * STAGE + RED + PRM);   // [in scale | in shift]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WGN, wn = wave % WGN;
@@ -490,14 +476,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
     }
     __syncthreads();
   }
-  if constexpr (PRO) {
-    // the producer's per-channel BN scale / shift (padding channels: 0, so act(0) = 0 keeps them 0)
-    for (int c = tid; c < NTP_PRO_MAX_C; c += NTHR) {
-      ppr[c] = c < p.pro_c ? p.pro_sc[c] : 0.0f;
-      ppr[NTP_PRO_MAX_C + c] = c < p.pro_c ? p.pro_sh[c] : 0.0f;
-    }
-    __syncthreads();
-  }
 
   // ---- loader (runs ST-1 steps ahead of compute) ----
   // Raw-buffer LDS-DMA (buffer_load_dwordx4 ... lds): a lane whose im2col element lies outside
@@ -527,29 +505,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
   uint32_t a_msk[A_SLOTS];
   uint32_t b_base[B_SLOTS];
   int tap = 0, cc = 0, ld_kt = 0, ld_tile = lb;
-  // PRO: tap-validity masks of this lane's A rows in the tile being COMPUTED (the loader's a_msk
-  // runs up to ST - 1 k-tiles, possibly a tile, ahead)
-  uint32_t c_msk[PRO ? A_SLOTS : 1];
-  auto row_mask = [&](int t, int i) -> uint32_t {
-    const int m = (t / p.tiles_n) * BM + r0 + RPP * i;
-    if (m >= M) return 0u;
-    const uint32_t n = fdiv((uint32_t)m, dv_hw);
-    const uint32_t rem = (uint32_t)m - n * dv_hw.d;
-    const uint32_t oy = fdiv(rem, dv_w);
-    const uint32_t ox = rem - oy * dv_w.d;
-    const int y0 = (int)oy * p.stride - p.pad, x0 = (int)ox * p.stride - p.pad;
-    uint32_t msk = 0;
-#pragma unroll
-    for (int tt = 0; tt < KS * KS; ++tt) {
-      const int iy = y0 + tt / KS, ix = x0 + tt % KS;
-      if (iy >= 0 && iy < p.SH && ix >= 0 && ix < p.SW) msk |= 1u << tt;
-    }
-    return msk;
-  };
-  if constexpr (PRO) {
-#pragma unroll
-    for (int i = 0; i < A_SLOTS; ++i) c_msk[i] = row_mask(lb, i);
-  }
   auto setup_rows = [&](int t) {
     const int m0 = (t / p.tiles_n) * BM;
     const int n0 = (t % p.tiles_n) * BN;
@@ -591,7 +546,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
     cc = 0;
   };
   setup_rows(ld_tile);
-  constexpr int CENTRE = KS == 1 ? 0 : 4;
   auto issue = [&](int stage) {
     char* lds_a = smem + stage * STAGE + wv * 1024;
     char* lds_b = smem + stage * STAGE + BM * 128 + wv * 1024;
@@ -816,60 +770,7 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
     // past the B rows issue only the A loads)
     if (!B_PART || wv * 8 < BN) wait_tiles<NG, ST - 2>(ahead);
     else wait_tiles<A_SLOTS, ST - 2>(ahead);
-    if constexpr (PRO) {
-      __builtin_amdgcn_sched_barrier(0);   // keep the transform's temporaries out of the MFMA phase
-      // this lane's own A chunks of the landed stage (its covering vmcnt wait above makes its own
-      // LDS-DMA bytes visible to its ds_reads): x = act(z * sc + sh), the affine pass's formula.
-      // k-tile ckt of tile ctile: the lane's chunk is channel chunk lc of tap lt
-      const int kc = ckt * NT_KCH + (UNI ? 0 : q);
-      const int lt = (int)(((uint64_t)(uint32_t)kc * p.cpt_magic) >> 32);
-      const int lc = kc - lt * p.cpt + (UNI ? q : 0);
-      const bool kok = UNI || kc < Kc;
-      const bool st_ok = lt == CENTRE && (ctile % p.tiles_n) == 0;
-      const int row0 = (ctile / p.tiles_n) * BM + r0;
-      int bits = 0;
-#pragma unroll
-      for (int i = 0; i < A_SLOTS; ++i)
-        if (kok && ((c_msk[i] >> lt) & 1u)) bits |= (1 << i) | (st_ok ? (1 << (8 + i)) : 0);
-      if (bits & 0xff) {
-        const int c0 = lc * 8;
-        const float* psc = ppr + c0;
-        const float* psh = ppr + NTP_PRO_MAX_C + c0;
-        char* base = smem + stage * STAGE + wv * 1024 + lane * 16;
-        // one slot at a time, two channels at a time: few live registers next to the accumulators
-#pragma unroll 1
-        for (int i = 0; i < A_SLOTS; ++i) {
-          if (!((bits >> i) & 1)) continue;
-          u32x4 v = *reinterpret_cast<const u32x4*>(base + i * SLOT);
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            const float2 s2 = *reinterpret_cast<const float2*>(psc + 2 * j);
-            const float2 h2 = *reinterpret_cast<const float2*>(psh + 2 * j);
-            T t2[2];
-            const uint32_t wj = v[j];
-            __builtin_memcpy(t2, &wj, 4);
-            float a0 = (float)t2[0] * s2.x + h2.x;
-            float a1 = (float)t2[1] * s2.y + h2.y;
-            if (p.pro_act == YMS_ACT_SILU) {
-              a0 = silu_f(a0);
-              a1 = silu_f(a1);
-            }
-            t2[0] = (T)a0;
-            t2[1] = (T)a1;
-            uint32_t wo;
-            __builtin_memcpy(&wo, t2, 4);
-            v[j] = wo;
-          }
-          *reinterpret_cast<u32x4*>(base + i * SLOT) = v;
-          if ((bits >> (8 + i)) & 1)
-            *reinterpret_cast<u32x4*>(p.pro_x + ((long)(row0 + RPP * i) * p.pro_x_ld + p.pro_x_off + c0) * ES) = v;
-        }
-      }
-      lds_barrier();      // every wave's transformed chunks are written before any MFMA reads
-      __builtin_amdgcn_sched_barrier(0);
-    } else {
-      raw_barrier();
-    }
+    raw_barrier();
     if (g + ST - 1 < total) {
       int ns = stage + ST - 1;
       if (ns >= ST) ns -= ST;
@@ -880,12 +781,6 @@ __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams 
       epilogue(ctile, stage);
       ckt = 0;
       ctile += G;
-      if constexpr (PRO) {
-        if (ctile < ntiles) {
-#pragma unroll
-          for (int i = 0; i < A_SLOTS; ++i) c_msk[i] = row_mask(ctile, i);
-        }
-      }
     }
     if (++stage == ST) stage = 0;
   }
@@ -1367,7 +1262,7 @@ static void launch_persistent(K kernel, const NTParams& p, int bm, unsigned gy, 
   hipLaunchKernelGGL(kernel, dim3(gx, gy), dim3(nthr), 0, st, p);
 }
 
-template <typename T, int KS, int MODE, int EPI, bool UNI, bool PRO = false>
+template <typename T, int KS, int MODE, int EPI, bool UNI>
 static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st) {
   NTParams p = p0;
   // dgrad grids: one block per output tile by default.  The weight gradients run beside dgrad on
@@ -1382,11 +1277,11 @@ static void launch_ntp(const NTParams& p0, int cfg, unsigned gy, hipStream_t st)
   // (round 4, measured and dropped: 256 x 128 tiles of 8 waves with 64 x 64 wave tiles, 5-40 %
   // slower, and 128 x 128 tiles of 4 such waves, within +-5 %: profiles/r04b_conv_micro_v*.txt)
   if (cfg == 0) {
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2, PRO>, p, 128, gy, st, g.occ * mult, 512, stats);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 128, 2, 4, 2, UNI, 2>, p, 128, gy, st, g.occ * mult, 512, stats);
   } else if (cfg == 1) {
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3, PRO>, p, 128, gy, st, g.occ * mult, 512, stats);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 128, 64, 4, 2, 2, UNI, 3>, p, 128, gy, st, g.occ * mult, 512, stats);
   } else {
-    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2, PRO>, p, 256, gy, st, g.occ * mult, 512, stats);
+    launch_persistent(conv_ntp_kernel<T, KS, MODE, EPI, 256, 32, 8, 1, 2, UNI, 2>, p, 256, gy, st, g.occ * mult, 512, stats);
   }
 }
 
@@ -1414,13 +1309,6 @@ static void launch_nt(const NTParams& p0, int cfg, hipStream_t st) {
     dim3 grid((unsigned)(cdiv(p.M, 128) * p.tiles_n), gy);
     hipLaunchKernelGGL((conv_nt_kernel<T, KS, MODE, EPI, 128, 32, 4, 1, 3>), grid, dim3(256), 0, st, p);
   }
-}
-
-// training forward with the producer's BN + activation as an A-operand prologue (16-bit, stride 1)
-template <typename T, int KS>
-static void launch_ntp_pro(const NTParams& p, int cfg, hipStream_t st) {
-  if (p.cpt % NT_KCH == 0) launch_ntp<T, KS, MODE_FWD, EPI_STATS, true, true>(p, cfg, 1u, st);
-  else launch_ntp<T, KS, MODE_FWD, EPI_STATS, false, true>(p, cfg, 1u, st);
 }
 
 // raw-buffer source extent and the exact kc / cpt multiply-shift for the 16-bit loader
@@ -1665,51 +1553,6 @@ yms_status yms_conv_fwd(const yms_conv_shape* s, const void* x, int x_ld, int x_
   hipStream_t st = (hipStream_t)stream;
   if (stats) return dispatch_nt<MODE_FWD, EPI_STATS>(p, s->dtype, s->k, tc.cfg, st);
   return dispatch_nt<MODE_FWD, EPI_AFFINE>(p, s->dtype, s->k, tc.cfg, st);
-}
-
-yms_status yms_conv_fwd_pro(const yms_conv_shape* s, const void* z, int z_ld, int z_off, const float* in_scale,
-                            const float* in_shift, int in_act, void* x, int x_ld, int x_off, const void* wpacked,
-                            void* y, int y_ld, int y_off, float* stats, void* stream) {
-  if (!yms_conv_fwd_pro_supported(s) || !z || !in_scale || !in_shift || !x || !wpacked || !y || !stats)
-    return !shape_ok(s) ? YMS_ERR_INVALID : YMS_ERR_UNSUPPORTED;
-  if (!view_ok(z_ld, z_off, s->cin) || !view_ok(x_ld, x_off, s->cin) || !view_ok(y_ld, y_off, s->cout))
-    return YMS_ERR_INVALID;
-  if (in_act != YMS_ACT_NONE && in_act != YMS_ACT_SILU) return YMS_ERR_INVALID;
-  PackGeo g = pack_geo(s, 0);
-  NTParams p{};
-  p.src = (const char*)z;
-  p.wp = (const char*)wpacked;
-  p.dst = (char*)y;
-  p.src_ld = z_ld; p.src_off = z_off; p.dst_ld = y_ld; p.dst_off = y_off;
-  p.act = YMS_ACT_NONE;
-  p.stats = stats;
-  p.stats_ld = (int)rup(s->cout, 128);
-  p.stats_cnt = stats + (long)yms_conv_stats_rows(s) * 2 * p.stats_ld;
-  p.SH = s->h; p.SW = s->w; p.OW = s->wo;
-  if (!offsets32(s->n, s->h, s->w, z_ld) || !offsets32(s->n, s->h, s->w, x_ld)) return YMS_ERR_UNSUPPORTED;
-  p.stride = s->stride; p.pad = s->pad;
-  p.cpt = g.cpt; p.Kc = g.kc; p.nkt = g.nkt;
-  if (!set_src_geometry(p, s->n, s->h, s->w, z_ld, 2, g.nkt * NT_KCH)) return YMS_ERR_UNSUPPORTED;
-  p.M = s->n * s->ho * s->wo;
-  p.Ncols = s->cout;
-  p.div_ow = make_fastdiv(s->wo);
-  p.div_ohw = make_fastdiv(s->ho * s->wo);
-  p.pro_sc = in_scale; p.pro_sh = in_shift; p.pro_act = in_act;
-  p.pro_x = (char*)x; p.pro_x_ld = x_ld; p.pro_x_off = x_off; p.pro_c = s->cin;
-  const TileChoice tc = choose_tile(s->cout);
-  hipStream_t st = (hipStream_t)stream;
-  if (s->dtype == YMS_BF16) {
-    launch_ntp_pro<bf16, 1>(p, tc.cfg, st);
-  } else {
-    launch_ntp_pro<f16, 1>(p, tc.cfg, st);
-  }
-  return launch_status();
-}
-
-int yms_conv_fwd_pro_supported(const yms_conv_shape* s) {
-  // 1x1 consumers only (3x3 consumers measured +1.7 ms per step: profiles/r04c_pro_ab.txt)
-  return shape_ok(s) && s->k == 1 && s->dtype != YMS_F32 && s->stride == 1 && s->pad == 0 && s->cin <= NTP_PRO_MAX_C &&
-         s->cin % 8 == 0 && s->ho == s->h && s->wo == s->w;
 }
 
 yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,

@@ -1278,15 +1278,12 @@ static int dw_occ(const yms_dw_shape* s) {
 // per block, 512 threads) for k = 3 when C is a multiple of 64, 7 (56 channels) for k = 3 when C is a
 // multiple of 56 but not of 32, else 4 (32 channels: the other part of each line is read and written
 // by the neighbouring blocks, on the same XCD).
-#ifndef DW_G7
-#define DW_G7 1   // dev A/B switch (0: 32-channel blocks)
-#endif
 static int dw_fwd_g(const yms_dw_shape* s) {
   if (s->k != 3 || s->dtype == YMS_F32) return 4;
   if (s->c % 64 == 0) return 8;
   // 56-channel blocks (448 threads) where 32-channel blocks would leave lanes idle: C = 112, 168, ...
   // (k3@160 c112 fwd 306 -> 282 us, dgrad 289 -> 253 us; profiles/r05ze_dw_g7_ab.txt)
-  return DW_G7 && s->c % 32 != 0 && s->c % 56 == 0 ? 7 : 4;
+  return s->c % 32 != 0 && s->c % 56 == 0 ? 7 : 4;
 }
 
 // forward / dgrad grid: image column tiles split into strips of tps tiles.  The strip length is
@@ -1394,9 +1391,6 @@ static bool dw_wgm(const yms_dw_shape* s) {
 struct DwWgmCfg {
   int nch, nb, nj, ncg, upb, groups;
 };
-#ifndef DW_WGM_NB2
-#define DW_WGM_NB2 1   // dev A/B switch (0: 16-row units only)
-#endif
 // units = (image, 16 dz rows; 32 for maps of 17-32 rows and one column chunk); 16 channels per block (512 threads, one block per CU: 8 waves of
 // ~220 VGPRs; 32-B pixel pieces per block, measured 4-8 % faster on k = 7 than 8-channel blocks at
 // two per CU, equal on k = 9); units per block: the fewest that keep the grid within one round of
@@ -1405,7 +1399,7 @@ static DwWgmCfg dw_wgm_cfg(const yms_dw_shape* s) {
   DwWgmCfg c;
   c.nch = (s->w + 31) / 32;
   // maps of 17-32 rows and one column chunk: both 16-row dz blocks in one unit (one staging)
-  c.nb = DW_WGM_NB2 && c.nch == 1 && s->h > 16 && s->h <= 32 ? 2 : 1;
+  c.nb = c.nch == 1 && s->h > 16 && s->h <= 32 ? 2 : 1;
   c.nj = (s->h + 16 * c.nb - 1) / (16 * c.nb);
   c.ncg = (s->c + DW_WGM_CG - 1) / DW_WGM_CG;
   const long units = (long)s->n * c.nj, slots = (DW_WGM_CG == 8 ? 2l : 1l) * conv_cu_count();

@@ -35,9 +35,11 @@ struct DecodeParams {
   int* label;
 };
 
-// 16 lanes per anchor: lanes 0..3 each own one DFL side (16 contiguous bins), all 16 lanes
-// stride over the classes, so the 64+nc logits of an anchor are read and its 4+nc outputs
-// written as contiguous lane-consecutive segments (NHWC makes an anchor's logits contiguous).
+// 16 lanes per anchor: lane 4*side + q owns bins 4q .. 4q+3 of DFL side `side` (the side's softmax
+// max / sums combine over its 4 lanes by xor shuffles, and lanes base + 0 / 4 / 8 / 12 then hold the
+// four distances); all 16 lanes stride over the classes, so the 64+nc logits of an anchor are read
+// and its 4+nc outputs written as contiguous lane-consecutive segments (NHWC makes an anchor's
+// logits contiguous).
 template <typename T>
 __global__ __launch_bounds__(256) void head_decode_kernel(DecodeParams p) {
   const int sub = threadIdx.x & 15;
@@ -774,15 +776,6 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
     // this block's tests); compaction only writes slots < blk + 64, so the prefetch is safe
     float4 cb_nx = lane < n ? boxes[lane] : make_float4(0.f, 0.f, 0.f, 0.f);
     int cid_nx = lane < n ? idx[lane] : 0;
-#ifdef YMS_NMS_PROF
-    // dev instrumentation (make -C yolo-ms_amd/csrc nmsprof; tools/nms_prof_run.py): wave 0's
-    // cycles per step phase, printed for the segments of image 0
-    long long pacc[6] = {0, 0, 0, 0, 0, 0}, pt = clock64();
-    int nres = 0;
-#define PMARK(k) do { if (tid == 0) { const long long q_ = clock64(); pacc[k] += q_ - pt; pt = q_; } } while (0)
-#else
-#define PMARK(k) do {} while (0)
-#endif
     for (int blk = 0; blk < n; blk += 64) {
       const int m = min(64, n - blk);
       const bool has = lane < m;
@@ -833,9 +826,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
       }
       const unsigned long long sm = __ballot(sup);
       if (lane == 0) s_sup[wave] = sm;
-      PMARK(0);
       lds_barrier();
-      PMARK(1);
       if (wave == 0) {
         unsigned long long allsup = 0;
 #pragma unroll
@@ -855,10 +846,6 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
           if (alive && lane > i && iou_gt_f(bi, cb, thr_f, full)) alive = false;
           am = __ballot(alive);
         }
-        PMARK(2);
-#ifdef YMS_NMS_PROF
-        nres += __popcll(done);
-#endif
         const int pos = nk + __popcll(am & ((1ull << lane) - 1ull));
         bool link = false;
         if (alive) {          // pos <= blk + lane: only already-consumed slots are overwritten
@@ -876,9 +863,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
       }
       // kept boxes past the LDS mirror are read back from global by the fallback path: only then
       // do the global stores above need the full barrier
-      PMARK(3);
       if (nk + 64 > NMS_KEPT_LDS) __syncthreads(); else lds_barrier();
-      PMARK(4);
       if (use_grid) {       // block-uniform: link the new kept boxes, cells split over the waves
         if (s_base[lane]) {
           const int pos = s_pos[lane];
@@ -892,15 +877,7 @@ __global__ __launch_bounds__(1024) void nms_big_greedy_kernel(int A, int nc, flo
         }
         lds_barrier();
       }
-      PMARK(5);
     }
-#ifdef YMS_NMS_PROF
-    if (tid == 0 && b == 0)
-      printf("NMSPROF seg n=%d kept=%d grid=%d gx=%d gy=%d ovf=%d resolved=%d test=%lld bar1=%lld "
-             "resolve=%lld write=%lld bar2=%lld insert=%lld\n", n, s_nk, (int)grid, gx, gy, s_ovf, nres,
-             pacc[0], pacc[1], pacc[2], pacc[3], pacc[4], pacc[5]);
-#endif
-#undef PMARK
     if (tid == 0) ws.cls_cnt[(long)b * nc + c] = s_nk;
     __syncthreads();
   }
@@ -1384,13 +1361,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
   __shared__ int s_wk[64], s_win[64];
   __shared__ unsigned long long s_wm[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-#ifdef YMS_NMS_PROF
-  long long wacc[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wpt = 0;
-  int nwin = 0;
-#define WMARK(k) do { if (tid == 0) { const long long q_ = clock64(); wacc[k] += q_ - wpt; wpt = q_; } } while (0)
-#else
-#define WMARK(k) do {} while (0)
-#endif
   const int nbig = ws.big[0];
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
     const int b = ws.big[1 + 2 * it], c = ws.big[2 + 2 * it];
@@ -1402,10 +1372,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
     int* idx = ws.scratch + (long)b * A + off;
     if (tid == 0) { s_bad = 0; s_nk = 0; }
     __syncthreads();
-#ifdef YMS_NMS_PROF
-    if (tid == 0) wpt = clock64();
-    nwin = 0;
-#endif
     // the segment's (unsorted) keys and boxes in registers: route statistics first
     float mnx = INFINITY, mxx = -INFINITY, mny = INFINITY, mxy = -INFINITY, wm = 0.0f, hm = 0.0f, ar = 0.0f;
     bool bad = false;
@@ -1484,7 +1450,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         continue;
       }
     }
-    WMARK(7);
     // sort the keys in LDS (priority order), then the sorted anchors to idx and boxes to s_box
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1495,11 +1460,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
     // merge sort with the region behind the keys as scratch (the rest of s_box, s_items and
     // s_kept: 64 KB, none of it live before the binning)
     msort8192(s_keys, s_keys + 8192, n);              // ends with a barrier (bitonic: +21 us per call)
-#ifdef YMS_NMS_PROF
-    WMARK(3);
-    const long long sortc = wacc[3];
-    wacc[3] = 0;
-#endif
     uint32_t av[PER];
 #pragma unroll
     for (int k = 0; k < PER; ++k) {
@@ -1535,7 +1495,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
       g.wmax = wm; g.hmax = hm; g.gx = gx; g.gy = gy;
     }
     const int ncell = g.gx * g.gy;
-    WMARK(0);
     // bin the positive-area boxes by centre (non-positive-area boxes never suppress or get suppressed)
     for (int i = tid; i < n; i += 1024) {
       const float4 q = s_box[i];
@@ -1568,7 +1527,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
     }
     if (tid == 0) s_cut = -1;
     __syncthreads();
-    WMARK(1);
     const int nwords = (n + 31) >> 5;                 // <= NMS_WG_MAX / 32 = 224 <= 4 * 64
     for (;;) {
       // 1. window (wave 0 alone, no cross-wave scan): the first 64 alive boxes after the cursor;
@@ -1600,10 +1558,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
       __syncthreads();
       const int m = __builtin_amdgcn_readfirstlane(s_m);
       if (m == 0) break;                              // block-uniform
-#ifdef YMS_NMS_PROF
-      ++nwin;
-#endif
-      WMARK(4);
       // 2. pairwise suppression bits of the window, one ballot per row: s_wm[t] bit l = member t
       //    (higher priority) suppresses member l > t; each lane's own member box loaded once
       {
@@ -1616,7 +1570,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         }
       }
       __syncthreads();
-      WMARK(6);
       // 3. serial greedy on the bit rows (wave 0, scalar), visiting only the members still alive:
       //    row t clears bits above t only, so jumping to the next alive member is the same walk
       if (wave == 0) {
@@ -1646,7 +1599,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         }
       }
       __syncthreads();
-      WMARK(2);
       // 4. every window survivor clears the alive bit of each later box of its search rectangle it
       //    suppresses; two candidates per lane and step, loads of both issued before either test
       //    (round 5, measured and dropped: the rectangle's rows flattened into one candidate index
@@ -1674,7 +1626,6 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         }
       }
       __syncthreads();
-      WMARK(3);
     }
     {
       // keep list -> anchor ids, in place over idx (all reads before the barrier, then the writes)
@@ -1692,21 +1643,12 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
         if (e < nk) idx[e] = av[k];
       }
     }
-#ifdef YMS_NMS_PROF
-    if (tid == 0 && b < 2) {
-      printf("WGRIDPROF b=%d c=%d n=%d kept=%d windows=%d gx=%d gy=%d load=%lld bin=%lld window=%lld bits=%lld serial=%lld suppress=%lld\n",
-             b, c, n, s_nk, nwin, g.gx, g.gy, wacc[0], wacc[1], wacc[4], wacc[6], wacc[2], wacc[3]);
-      printf("WGRIDPROF2 b=%d c=%d route=%lld sort=%lld\n", b, c, wacc[7], sortc);
-    }
-    for (int k = 0; k < 8; ++k) wacc[k] = 0;
-#endif
     if (tid == 0) {
       ws.cls_cnt[(long)b * nc + c] = s_nk;
       ws.route[(long)b * nc + c] = 2;                 // done: the kept-list greedy skips it
     }
     __syncthreads();
   }
-#undef WMARK
 }
 
 // The window-grid greedy for sorted segments too big for LDS (NMS_WG_MAX < n <= NMS_WGG_MAX, finite,

@@ -60,9 +60,8 @@ _SIGS = {
     "yms_conv_pack_weights_batched": (_I, [_I, _P, _P, _P]),
     "yms_conv_stats_rows": (_I, [_SP]),
     "yms_conv_stats_ld": (_I, [_SP]),
+    "yms_conv_direct_set": (_I, [_I]),
     "yms_conv_fwd": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _P]),
-    "yms_conv_fwd_pro_supported": (_I, [_SP]),
-    "yms_conv_fwd_pro": (_I, [_SP, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _P, _I, _I, _P, _P]),
     "yms_conv_stem_supported": (_I, [_SP]),
     "yms_conv_stem_stats_rows": (_I, [_SP]),
     "yms_conv_stem_fwd": (_I, [_SP, _P, _P, _P, _I, _I, _P, _P, _I, _P, _I, _P]),
@@ -145,7 +144,7 @@ def check(status, what):
 
 
 _prof = None
-_CONV = ("yms_conv_fwd", "yms_conv_fwd_pro", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd")
+_CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd")
 _DW = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
 # launches whose hipStream_t is the last argument (status-returning entry points ending in a void*)
 # (host-only entry points whose last pointer is a host buffer are listed out explicitly)
@@ -169,8 +168,7 @@ def _work(name, args):
         sh = args[0].contents
         fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
         es = _elt(sh.dtype)
-        nin = 2 if name == "yms_conv_fwd_pro" else 1        # pro: reads z, writes the producer's x
-        act = (nin * sh.n * sh.h * sh.w * sh.cin + sh.n * sh.ho * sh.wo * sh.cout) * es
+        act = (sh.n * sh.h * sh.w * sh.cin + sh.n * sh.ho * sh.wo * sh.cout) * es
         return fl, act + sh.cout * sh.cin * sh.k * sh.k * (4 if name == "yms_conv_wgrad" else es)
     if name in _DW:
         d = args[0].contents

@@ -5,6 +5,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 import torch
 
@@ -29,23 +30,31 @@ def dfl(x, ch=16):
     return out
 
 
-_WS = {}
+_TLS = threading.local()
 
 
 def _nms_ws(dev, B, A, nc, iou):
-    """NMS scratch reused across calls on one stream (calls on a stream are ordered, so one buffer
-    per (device, stream) is safe; a call on another stream gets its own)."""
+    """NMS scratch reused across calls, one buffer per (host thread, device, stream): one
+    yms_nms_classwise call is a chain of launches on its stream (memset, route / sort, greedy,
+    compact), so two threads sharing a stream would interleave their chains over one buffer
+     -- a thread's own calls on a stream are ordered, so its buffer is safe to reuse.
+    The cache lives in thread-local storage and goes with the thread."""
     # graph NMS (csrc/head_nms.hip) runs on segments of at least YMS_NMS_GRAPH_MIN boxes (default
     # 2048, 0 = off, at least 32, the C side's rule); without it the workspace leaves out the graph
     # kernels' suppressee lists (~530 B per anchor) and every segment takes the other exact routes
     gmin = int(os.environ.get("YMS_NMS_GRAPH_MIN", "2048"))
     full = iou >= 0.0 and gmin > 0 and A >= max(gmin, 32)
     nbytes = (L.lib().yms_nms_ws_bytes if full else L.lib().yms_nms_ws_bytes_min)(B, A, nc)
+    cache = getattr(_TLS, "nms_ws", None)
+    if cache is None:
+        cache = _TLS.nms_ws = {}
     key = (dev.index, L.stream_ptr(dev))
-    ws = _WS.get(key)
+    ws = cache.get(key)
     if ws is None or ws.numel() < nbytes:
+        if len(cache) >= 8:            # a thread cycling through many streams: keep a few
+            cache.pop(next(iter(cache)))
         ws = torch.empty(nbytes, dtype=torch.uint8, device=dev)
-        _WS[key] = ws
+        cache[key] = ws
     return ws, nbytes
 
 

@@ -240,8 +240,6 @@ class ConvOp:
         self.pb = b.param(mod.bn, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
-        self.pro_by = None       # consumer conv that forms (and stores) this op's x = act(BN(z))
-        self.pro = None          # producer whose act(BN(z)) this conv forms in its prologue
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -315,11 +313,6 @@ class ConvOp:
         if stem:
             L.call("yms_conv_stem_fwd", self.sp, rt.stem_x[self.stem_input].data_ptr(), m.conv.weight.data_ptr(),
                    base + self.z, self.zld, 0, None, None, L.ACT_NONE, stats, self.stats_ld, rt.st)
-        elif self.pro is not None:
-            # the producer's affine pass is folded in: read its z, form x in the prologue and store it
-            q = self.pro
-            L.call("yms_conv_fwd_pro", self.sp, base + q.z, q.zld, 0, base + q.sc, base + q.sh, q.act, rt.a(x), xl,
-                   x.off, base + self.t_wp, base + self.z, self.zld, 0, stats, rt.st)
         else:
             L.call("yms_conv_fwd", self.sp, rt.a(x), xl, x.off, base + self.t_wp, base + self.z, self.zld, 0,
                    None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
@@ -328,9 +321,8 @@ class ConvOp:
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
-        if self.pro_by is None:
-            L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
-                   base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
+        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+               base + self.sh, self.act, rp, rl, ro, rt.a(y), yl, y.off, rt.st)
 
     def plan_grads(self, T):
         T.read(self.y)
@@ -478,7 +470,6 @@ class DWConvOp(ConvOp):
         self.pb = b.param(mod.bn, "bias")
         self.flops = 0          # not an MFMA contraction: excluded from the conv roofline
         self.dw_flops = 2 * self.npix * c * k * k
-        self.pro_by = None      # consumer conv that forms (and stores) this op's output in its prologue
 
     def layout(self, plan, La, Le):
         es, c = plan.es, self.c
@@ -526,9 +517,8 @@ class DWConvOp(ConvOp):
                bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
                ctypes.c_float(bn.eps), base + self.mi, base + self.sc, base + self.sh, rt.st)
-        if self.pro_by is None:
-            L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
-                   base + self.sh, self.act, None, 0, 0, rt.a(y), y.buf.ld, y.off, rt.st)
+        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+               base + self.sh, self.act, None, 0, 0, rt.a(y), y.buf.ld, y.off, rt.st)
 
     def bwd(self, rt):
         x, y = self.x, self.y
@@ -726,7 +716,6 @@ class Plan:
         self.scratch_req = {}
         self.n_counters = 0
         self.stem_inputs = self._find_stems()
-        self._find_pro()
         La, Le = Layout(), Layout()
         for buf in self.bufs:
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
@@ -789,51 +778,6 @@ class Plan:
                 op.stem_input = i
                 out[i] = op
         return out
-
-    def _find_pro(self):
-        """Training, 16-bit: a Conv op whose input view is exactly the output of one earlier Conv /
-        depthwise op (no residual in that op's affine pass) and which is the FIRST reader of it
-        takes the producer's BN + activation as an A-operand prologue (yms_conv_fwd_pro): it reads
-        the producer's z, forms x = act(z * scale + shift) in LDS and stores x from its centre-tap
-        tiles, so the producer's affine pass goes (its write stays, its read of z is the conv's own
-        input read).  x is still materialised, so every later reader and the whole backward are
-        unchanged.  Stride-1 'same' consumers only (their centre tap covers every input pixel once).
-        Opt-in (YMS_PRO=1), 1x1 consumers only (3x3 consumers transform every input element once
-        per tap: YOLOv8-s 18.8 -> 20.5 ms/step with them, profiles/r04c_pro_ab.txt): the bytes it
-        removes (the affine pass's z read) do not pay for the prologue conv's lower occupancy --
-        interleaved on one box, YOLOv8-s 18.36 vs 18.38 ms/step and YOLO-MS-S 35.83 vs 36.75 ms/step,
-        off vs on (profiles/r04q_pro_1x1_ab.txt)."""
-        if not self.training or self.dt == L.F32 or os.environ.get("YMS_PRO", "0") == "0":
-            return
-        for i, c in enumerate(self.ops):
-            if type(c) is not ConvOp or c.stem_input is not None:
-                continue
-            if not L.lib().yms_conv_fwd_pro_supported(c.sp):
-                continue
-            x = c.x
-            prod = None
-            for j in range(i - 1, -1, -1):
-                q = self.ops[j]
-                y = getattr(q, "y", None)
-                if isinstance(y, View) and y.buf is x.buf and not (y.off + y.c <= x.off or x.off + x.c <= y.off):
-                    prod = (j, q)
-                    break
-            if prod is None:
-                continue
-            j, q = prod
-            if type(q) not in (ConvOp, DWConvOp) or q.y.off != x.off or q.y.c != x.c or q.res is not None:
-                continue
-            if q.pro_by is not None or q.act not in (L.ACT_NONE, L.ACT_SILU):
-                continue
-            if getattr(q, "stem_input", None) is not None:
-                continue
-            # no op between producer and consumer reads the producer's output
-            between = self.ops[j + 1:i]
-            if any(isinstance(a, View) and a.buf is x.buf and not (a.off + a.c <= x.off or x.off + x.c <= a.off)
-                   for op in between for k, a in vars(op).items() if k != "y"):
-                continue
-            q.pro_by = c
-            c.pro = q
 
     def counter(self):
         """Reserve one 16-B arrival counter in the grad scratch (-> its index)."""

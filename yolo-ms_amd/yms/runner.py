@@ -262,6 +262,9 @@ class _PlanFn(torch.autograd.Function):
         return (None, *in_grads, *views)
 
 
+_INFER_ARENAS_MAX = 4
+
+
 def run(module, inputs, grad_hook=None):
     """Execute `module` on `inputs` (list of NCHW cuda tensors) through its plan."""
     _check_inputs(inputs)
@@ -287,17 +290,21 @@ def run(module, inputs, grad_hook=None):
         # thread) -- the next call from that thread on that stream is ordered after this one, while
         # two threads sharing a stream would interleave their launches -- and skip
         # re-zeroing the pad ranges
+        # (bounded -- the oldest entry goes once a plan holds _INFER_ARENAS_MAX, so a
+        # thread pool churning through threads does not keep one full arena per dead thread)
         arena = None
         if decode:
             cache = plan.__dict__.setdefault("_infer_arenas", {})
             key = (stream, threading.get_ident())
-            arena = cache.get(key)
+            arena = cache.pop(key, None)
             if arena is not None and arena.device != dev:
                 arena = None
         if arena is None:
             arena = plan.new_arena(dev, stream)
-            if decode:
-                cache[key] = arena
+        if decode:
+            while len(cache) >= _INFER_ARENAS_MAX:
+                cache.pop(next(iter(cache)))
+            cache[key] = arena           # re-inserted last: the dict's order is least-recently used first
         rt = Rt(plan, arena.data_ptr(), stream, False)
         rt.eval_base = plan.ensure_eval_cache(dev, stream)
         _load_inputs(plan, rt, inputs)
