@@ -77,6 +77,10 @@ typedef struct {
   const float* w;
   void* packed;
   int cout, cin, ks, rows, kp_elems, c8_in, for_dgrad, dtype;
+  /* optional second source (sibling convs packed as one, yms_pack_job_init sets NULL / 0): output
+   * channels co >= split read w2[co - split] instead of w[co] */
+  const float* w2;
+  int split;
 } yms_pack_job;
 yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* packed, int for_dgrad,
                              yms_pack_job* job);
@@ -145,6 +149,13 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
                            const float* gamma, const float* beta, float* rmean, float* rvar,
                            float momentum, float eps, float* mean_invstd, float* scale,
                            float* shift, void* stream);
+/* The same with the invstd row of mean_invstd mi_ld floats after the mean row (>= c): the channel
+ * slice of a wider [2][mi_ld] table, for sibling convs whose outputs are slots of one buffer and
+ * share one BN backward pass over all their channels (yolov8_head.py:84-85, 99-100). */
+yms_status yms_bn_finalize_ld(int c, float* stats, int rows, int stats_ld, long count,
+                              const float* gamma, const float* beta, float* rmean, float* rvar,
+                              float momentum, float eps, float* mean_invstd, int mi_ld, float* scale,
+                              float* shift, void* stream);
 /* y = act(z*scale + shift) (+ res), over npix pixels x c channels. */
 yms_status yms_affine_act(int dtype, long npix, int c, const void* z, int z_ld, int z_off,
                           const float* scale, const float* shift, int act,

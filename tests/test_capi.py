@@ -83,9 +83,43 @@ def test_plan_construction_s640():
         m.train(tr)
         p = runner.get_plan(m, [x], torch.bfloat16, tr)
         assert abs(p.flops / 4 / 1e9 - 25.79) < 0.01
-        assert len(p.ops) == 66
+        # 66 modules' ops, the head's three box[i][0] / cls[i][0] pairs as one SiblingConvOp each
+        assert len(p.ops) == 63
     with pytest.raises(RuntimeError, match="multiple of 32"):
         runner.get_plan(m, [torch.empty(1, 3, 100, 100, device="meta")], torch.float32, False)
+
+
+def test_sibling_head_convs_plan(monkeypatch):
+    """The head's box[i][0] / cls[i][0] pair (yolov8_head.py:84-85, 99-100) is one SiblingConvOp in a
+    16-bit plan: outputs in the slots [0, 64) / [64, 64 + nc) of one buffer, members' parameter
+    gradients adjacent in the flat arena (bias, gamma, weight kinds in turn), the same parameter set
+    and FLOPs as the unfused plan (YMS_HEAD_FUSE=0 keeps two ConvOps)."""
+    from yms import runner
+    from yms.plan import SiblingConvOp
+    from yolov8.yolov8 import YOLOv8
+    m = YOLOv8("s", 20)
+    x = torch.empty(2, 3, 256, 256, device="meta")
+    m.train(True)
+    p = runner.get_plan(m, [x], torch.bfloat16, True)
+    sib = [op for op in p.ops if isinstance(op, SiblingConvOp)]
+    assert len(sib) == 3
+    for i, op in enumerate(sib):
+        a, b = op.members
+        assert a.mod is m.head.box[i][0] and b.mod is m.head.cls[i][0]
+        assert (a.y.off, a.y.c, b.y.off, b.y.c, op.c) == (0, 64, 64, 20, 84) and a.y.buf is b.y.buf
+        assert op.shape.cout == 84 and op.shape.cin == a.shape.cin and op.flops == a.flops + b.flops
+        order = p.pgrad_order
+        for kind in ("pb", "pg", "pw"):
+            ia, ib = order.index(getattr(a, kind)), order.index(getattr(b, kind))
+            assert ib == ia + 1
+    p3 = runner.get_plan(m, [x], torch.float32, True)
+    assert sum(isinstance(op, SiblingConvOp) for op in p3.ops) == 3
+    monkeypatch.setenv("YMS_HEAD_FUSE", "0")
+    m2 = YOLOv8("s", 20)
+    m2.train(True)
+    p2 = runner.get_plan(m2, [x], torch.bfloat16, True)
+    assert not any(isinstance(op, SiblingConvOp) for op in p2.ops) and len(p2.ops) == len(p.ops) + 3
+    assert p2.flops == p.flops and len(p2.param_refs) == len(p.param_refs)
 
 
 def test_state_dict_keys_identical_to_reference():

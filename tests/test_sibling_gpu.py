@@ -1,0 +1,58 @@
+"""The head's sibling first convs (yolov8_head.py:84-85, 99-100: box[i][0] and cls[i][0] both read
+x_i) run as one SiblingConvOp (yms/plan.py): outputs in the slots of one buffer, one BN backward
+pass, one input gradient and one weight gradient over both.  Checked against the unfused plan
+(YMS_HEAD_FUSE=0, one ConvOp per module) on the same weights and batch: the forward maps and the BN
+running buffers are bit-identical (each member's conv, statistics and finalize are unchanged; the
+affine pass is elementwise), and the parameter gradients agree to the accumulation-order rounding
+(fp32: the reduce's per-block pixel order differs with the channel count; 16-bit: the unfused
+input gradient rounds dx twice, store then accumulate).  The fused fp32 path is also covered by
+every fp32 oracle / golden model test, which run it by default."""
+import pytest
+import torch
+
+from yms import set_compute_dtype
+from yms.plan import SiblingConvOp
+from yolov8.yolov8 import YOLOv8
+
+pytestmark = pytest.mark.gpu
+
+
+def _step(fuse, dtype, version, nc, x, sd, monkeypatch):
+    monkeypatch.setenv("YMS_HEAD_FUSE", "1" if fuse else "0")
+    m = YOLOv8(version, nc).cuda()
+    m.load_state_dict(sd)
+    m.train()
+    if dtype != torch.float32:
+        set_compute_dtype(m, dtype)
+    outs = m(x)
+    plans = list(m.__dict__["_yms_plans"].values())
+    assert any(isinstance(op, SiblingConvOp) for op in plans[0].ops) == fuse
+    g = torch.Generator(device="cuda").manual_seed(3)
+    loss = sum((o.float() * torch.randn(o.shape, device="cuda", generator=g)).sum() for o in outs)
+    loss.backward()
+    torch.cuda.synchronize()
+    grads = {k: p.grad.detach().float().clone() for k, p in m.named_parameters() if p.grad is not None}
+    bufs = {k: b.detach().clone() for k, b in m.named_buffers()}
+    return [o.detach().float().clone() for o in outs], grads, bufs
+
+
+@pytest.mark.parametrize("dtype,tol", [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+@pytest.mark.parametrize("version,nc,size", [("s", 80, 256), ("n", 3, 192), ("ms-s", 80, 256)])
+def test_sibling_head_convs_match_unfused(dtype, tol, version, nc, size, monkeypatch):
+    torch.manual_seed(0)
+    sd = YOLOv8(version, nc).state_dict()
+    x = torch.randn(2, 3, size, size, generator=torch.Generator().manual_seed(1)).cuda()
+    o1, g1, b1 = _step(True, dtype, version, nc, x, sd, monkeypatch)
+    o0, g0, b0 = _step(False, dtype, version, nc, x, sd, monkeypatch)
+    for a, b in zip(o1, o0):
+        assert torch.equal(a, b)
+    for k in b0:
+        assert torch.equal(b1[k], b0[k]), k
+    assert g1.keys() == g0.keys()
+    worst = 0.0
+    for k in g0:
+        d = ((g1[k] - g0[k]).norm() / (g0[k].norm() + 1e-30)).item()
+        worst = max(worst, d)
+        assert d <= tol, (k, d)
+    # the head's own parameters (the fused ones) must actually have been exercised
+    assert any(k.startswith("head.cls.0.0") for k in g0)

@@ -116,7 +116,8 @@ constexpr int FIN_CW = 8, FIN_RL = 1024 / FIN_CW;
 __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* stats, int rows, int ld, int rs,
                                                            int rows_total, long count, const float* g,
                                                            const float* b, float* rm, float* rv, float momentum,
-                                                           float eps, float* mi, float* scale, float* shift) {
+                                                           float eps, float* mi, int mi_ld, float* scale,
+                                                           float* shift) {
   __shared__ double red[FIN_RL * (FIN_CW + 1)][4];
   const int tx = threadIdx.x % FIN_CW, ty = threadIdx.x / FIN_CW;
   const int ch = blockIdx.x * FIN_CW + tx;
@@ -161,7 +162,7 @@ __global__ __launch_bounds__(1024) void bn_finalize_kernel(int c, const float* s
     if (rm) rm[ch] = (float)((1.0 - momentum) * (double)rm[ch] + momentum * mean);
     if (rv) rv[ch] = (float)((1.0 - momentum) * (double)rv[ch] + momentum * uvar);
     mi[ch] = (float)mean;
-    mi[c + ch] = invstd;
+    mi[mi_ld + ch] = invstd;
     const float sc = g[ch] * invstd;
     scale[ch] = sc;
     shift[ch] = b[ch] - (float)mean * sc;
@@ -179,7 +180,7 @@ constexpr int FIN3_RL = 32;
 __global__ __launch_bounds__(256) void bn_finalize_small_kernel(int c, const float* stats, int rows, int ld,
                                                                 long count, const float* g, const float* b, float* rm,
                                                                 float* rv, float momentum, float eps, float* mi,
-                                                                float* scale, float* shift) {
+                                                                int mi_ld, float* scale, float* shift) {
   __shared__ double red[FIN3_RL * 9][4];
   const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
   const int ch = blockIdx.x * 8 + tx;
@@ -214,7 +215,7 @@ __global__ __launch_bounds__(256) void bn_finalize_small_kernel(int c, const flo
     if (rm) rm[ch] = (float)((1.0 - momentum) * (double)rm[ch] + momentum * mean);
     if (rv) rv[ch] = (float)((1.0 - momentum) * (double)rv[ch] + momentum * uvar);
     mi[ch] = (float)mean;
-    mi[c + ch] = invstd;
+    mi[mi_ld + ch] = invstd;
     const float sc = g[ch] * invstd;
     scale[ch] = sc;
     shift[ch] = b[ch] - (float)mean * sc;
@@ -946,13 +947,13 @@ yms_status yms_bn_fold(int c, const float* gamma, const float* beta, const float
   return launch_status();
 }
 
-yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
-                           const float* gamma, const float* beta, float* rmean, float* rvar,
-                           float momentum, float eps, float* mean_invstd, float* scale,
-                           float* shift, void* stream) {
+yms_status yms_bn_finalize_ld(int c, float* stats, int rows, int stats_ld, long count,
+                              const float* gamma, const float* beta, float* rmean, float* rvar,
+                              float momentum, float eps, float* mean_invstd, int mi_ld, float* scale,
+                              float* shift, void* stream) {
   if (c <= 0 || !stats || rows <= 0 || count <= 0 || !gamma || !beta || !mean_invstd || !scale || !shift)
     return YMS_ERR_INVALID;
-  if (stats_ld < c) return YMS_ERR_INVALID;
+  if (stats_ld < c || mi_ld < c) return YMS_ERR_INVALID;
   int rs = 1, nrows = rows;
   if (rows > 1024) {   // long tables: pre-reduce in parallel (in place), then finalize the partial rows
     const int S = std::min(256, cdiv(rows, 64));
@@ -964,13 +965,21 @@ yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long cou
   if (rs == 1) {
     hipLaunchKernelGGL(bn_finalize_small_kernel, dim3(cdiv(c, 8)), dim3(256), 0, (hipStream_t)stream, c,
                        (const float*)stats, rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps,
-                       mean_invstd, scale, shift);
+                       mean_invstd, mi_ld, scale, shift);
     return launch_status();
   }
   hipLaunchKernelGGL(bn_finalize_kernel, dim3(cdiv(c, FIN_CW)), dim3(1024), 0, (hipStream_t)stream, c,
                      (const float*)stats, nrows, stats_ld, rs, rows, count, gamma, beta, rmean, rvar, momentum,
-                     eps, mean_invstd, scale, shift);
+                     eps, mean_invstd, mi_ld, scale, shift);
   return launch_status();
+}
+
+yms_status yms_bn_finalize(int c, float* stats, int rows, int stats_ld, long count,
+                           const float* gamma, const float* beta, float* rmean, float* rvar,
+                           float momentum, float eps, float* mean_invstd, float* scale,
+                           float* shift, void* stream) {
+  return yms_bn_finalize_ld(c, stats, rows, stats_ld, count, gamma, beta, rmean, rvar, momentum, eps,
+                            mean_invstd, c, scale, shift, stream);
 }
 
 // pixels per block for the channel-stationary kernels: about four U-pixel iterations per

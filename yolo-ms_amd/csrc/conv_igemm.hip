@@ -1114,7 +1114,10 @@ __global__ __launch_bounds__(256) void pack_weight_batched_kernel(const yms_pack
       if (tap < kk) {
         const int co = j.for_dgrad ? c : r;
         const int ci = j.for_dgrad ? r : c;
-        if (co < j.cout && ci < j.cin) v = j.w[((long)co * j.cin + ci) * kk + tap];
+        if (co < j.cout && ci < j.cin) {
+          const bool hi = j.w2 && co >= j.split;
+          v = (hi ? j.w2 : j.w)[((long)(hi ? co - j.split : co) * j.cin + ci) * kk + tap];
+        }
       }
       const long o = (long)r * j.kp_elems + k;
       if (j.dtype == YMS_BF16) reinterpret_cast<bf16*>(j.packed)[o] = (bf16)v;
@@ -1449,6 +1452,8 @@ yms_status yms_pack_job_init(const yms_conv_shape* s, const float* w, void* pack
   job->c8_in = g.c8_in;
   job->for_dgrad = for_dgrad;
   job->dtype = s->dtype;
+  job->w2 = nullptr;
+  job->split = 0;
   return YMS_OK;
 }
 

@@ -39,7 +39,8 @@ class DwShape(ctypes.Structure):
 
 class PackJob(ctypes.Structure):
     _fields_ = [("w", ctypes.c_void_p), ("packed", ctypes.c_void_p)] + [
-        (k, ctypes.c_int) for k in ("cout", "cin", "ks", "rows", "kp_elems", "c8_in", "for_dgrad", "dtype")]
+        (k, ctypes.c_int) for k in ("cout", "cin", "ks", "rows", "kp_elems", "c8_in", "for_dgrad", "dtype")] + [
+        ("w2", ctypes.c_void_p), ("split", ctypes.c_int)]
 
 
 _P = ctypes.c_void_p
@@ -72,6 +73,7 @@ _SIGS = {
     "yms_conv_wgrad": (_I, [_SP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
     "yms_bn_fold": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
     "yms_bn_finalize": (_I, [_I, _P, _I, _I, _L, _P, _P, _P, _P, _F, _F, _P, _P, _P, _P]),
+    "yms_bn_finalize_ld": (_I, [_I, _P, _I, _I, _L, _P, _P, _P, _P, _F, _F, _P, _I, _P, _P, _P]),
     "yms_affine_act": (_I, [_I, _L, _I, _P, _I, _I, _P, _P, _I, _P, _I, _I, _P, _I, _I, _P]),
     "yms_bn_bwd_rows": (_I, [_L, _I]),
     "yms_bn_act_bwd_reduce": (_I, [_I, _L, _I, _P, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),

@@ -374,6 +374,163 @@ class ConvOp:
         return [self.pb, self.pg, self.pw]
 
 
+class SiblingConvOp:
+    """Two Conv blocks (Conv2d -> BN -> act, components.py:69-77) that read the SAME input view --
+    the head's box[i][0] and cls[i][0] (yolov8_head.py:84-85, 99-100: Conv(c_i, 4*ch) and
+    Conv(c_i, nc), both 3x3 of x_i) -- with their outputs as the two channel slots of one buffer
+    [.., c_a | c_b].  The forward runs each member's conv (its own tile shape) into its slot of one
+    z buffer and its own BN finalize; everything after is one pass over the c_a + c_b channels:
+    ONE affine pass; in the backward ONE BN reduce / finalize / apply, ONE input gradient (a single
+    GEMM with K = k^2 (c_a + c_b): dx is stored once instead of stored, re-read and accumulated by a
+    second dgrad) and ONE weight gradient (M = c_a + c_b).  The members' parameter gradients are
+    adjacent in the flat gradient arena (grad_params order), so the fused backward writes them in
+    place; the transposed dgrad weight is packed from both fp32 weights by one pack job (w2 / split)."""
+
+    def __init__(self, b, mods, x, y, act):
+        self.x, self.y, self.res, self.act = x, y, None, act
+        self.members, self.offs = [], []
+        off = 0
+        for m in mods:
+            self.offs.append(off)
+            self.members.append(ConvOp(b, m, x, y.slot(off, m.conv.out_channels), None, act))
+            off += m.conv.out_channels
+        self.c = off
+        m0 = self.members[0]
+        sh0 = m0.shape
+        self.shape = L.ConvShape(sh0.n, sh0.h, sh0.w, sh0.cin, self.c, sh0.k, sh0.stride, sh0.pad, sh0.ho, sh0.wo, sh0.dtype)
+        self.sp = ctypes.pointer(self.shape)
+        self.npix = m0.npix
+        self.flops = sum(m.flops for m in self.members)
+        self.stem_input = None
+
+    def layout(self, plan, La, Le):
+        es = plan.es
+        for m in self.members:
+            m.wp_elems = L.lib().yms_conv_packed_elems(m.sp, 0)
+            m.e_wp = Le.alloc(m.wp_elems * es)
+            m.e_sc = Le.alloc(4 * m.c)
+            m.e_sh = Le.alloc(4 * m.c)
+        if not plan.training:
+            return
+        c = self.c
+        self.zld = r8(c)
+        self.z = La.alloc(self.npix * self.zld * es)
+        for m in self.members:
+            m.t_wp = La.alloc(m.wp_elems * es)
+            m.stats_rows = L.lib().yms_conv_stats_rows(m.sp)
+            m.stats_ld = L.lib().yms_conv_stats_ld(m.sp)
+            plan.need_scratch("stats", 4 * m.stats_rows * (2 * m.stats_ld + 1))
+        self.wpt_elems = L.lib().yms_conv_packed_elems(self.sp, 1)
+        self.t_wpt = La.alloc(self.wpt_elems * es)
+        self.sc = La.alloc(4 * c)
+        self.sh = La.alloc(4 * c)
+        self.mi = La.alloc(8 * c)
+        self.bwd_rows = L.lib().yms_bn_bwd_rows(self.npix, c)
+        plan.need_scratch("bwd", 4 * 2 * c * self.bwd_rows)
+        plan.need_scratch("coef", 8 * c)
+        # the fallback when the members' parameter gradients are not adjacent (some frozen):
+        # dgamma / dbeta into scratch, then per member
+        plan.need_scratch("sib", 8 * c)
+        self.wg_ws = L.lib().yms_conv_wgrad_ws_bytes(self.sp)
+        plan.need_scratch("wgrad", self.wg_ws)
+        for m in self.members:
+            m.wg_ws = L.lib().yms_conv_wgrad_ws_bytes(m.sp)
+            plan.need_scratch("wgrad", m.wg_ws)
+
+    def pack_specs(self):
+        """(shape, fp32 weight, arena offset, for_dgrad[, (second weight, split)]) per pack."""
+        specs = [(m.sp, m.mod.conv.weight.data_ptr(), m.t_wp, 0) for m in self.members]
+        a, bb = self.members
+        specs.append((self.sp, a.mod.conv.weight.data_ptr(), self.t_wpt, 1,
+                      (bb.mod.conv.weight.data_ptr(), a.c)))
+        return specs
+
+    def prepare_eval(self, rt):
+        for m in self.members:
+            m.prepare_eval(rt)
+
+    def bn_modules(self):
+        return [m.mod for m in self.members]
+
+    def fwd(self, rt):
+        if not rt.training:
+            for m in self.members:      # eval: BN + act fused in each member's epilogue, into its slot
+                m.fwd(rt)
+            return
+        if not rt.prepacked:
+            raise RuntimeError("yms: sibling convs need the batched pack (Plan.prepack)")
+        x, y = self.x, self.y
+        base = rt.base
+        stats = base + rt.plan.scratch["stats"]
+        for m, off in zip(self.members, self.offs):
+            L.call("yms_conv_fwd", m.sp, rt.a(x), x.buf.ld, x.off, base + m.t_wp, base + self.z, self.zld, off,
+                   None, None, L.ACT_NONE, None, 0, 0, stats, rt.st)
+            bn = m.mod.bn
+            L.call("yms_bn_finalize_ld", m.c, stats, m.stats_rows, m.stats_ld, self.npix, bn.weight.data_ptr(),
+                   bn.bias.data_ptr(), bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                   ctypes.c_float(bn.momentum if bn.momentum is not None else BN_MOMENTUM),
+                   ctypes.c_float(bn.eps), base + self.mi + 4 * off, self.c, base + self.sc + 4 * off,
+                   base + self.sh + 4 * off, rt.st)
+        L.call("yms_affine_act", rt.plan.dt, self.npix, self.c, base + self.z, self.zld, 0, base + self.sc,
+               base + self.sh, self.act, None, 0, 0, rt.a(y), y.buf.ld, y.off, rt.st)
+
+    def plan_grads(self, T):
+        T.read(self.y)
+        self.acc_x = T.write(self.x) if self.x.buf.needs_grad else 0
+
+    def _adjacent(self, rt, attr):
+        ps = [rt.pgrad(getattr(m, attr)) for m in self.members]
+        if any(p is None for p in ps):
+            return None
+        for m, p, q in zip(self.members, ps, ps[1:]):
+            per = m.mod.conv.weight[0].numel() if attr == "pw" else 1
+            if q != p + 4 * per * m.c:
+                return None
+        return ps[0]
+
+    def bwd(self, rt):
+        x, y = self.x, self.y
+        base, dt, c = rt.base, rt.plan.dt, self.c
+        gy, gyl, gyo = rt.g(y), y.buf.ld, y.off
+        ws = rt.gbase + rt.plan.gscratch["bwd"]
+        coef = rt.gbase + rt.plan.gscratch["coef"]
+        z = base + self.z
+        L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+               base + self.sh, base + self.mi, self.act, ws, rt.st)
+        dg, db = self._adjacent(rt, "pg"), self._adjacent(rt, "pb")
+        if dg is not None and db is not None:
+            L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix, dg, db, coef, rt.st)
+        else:
+            tmp = rt.gbase + rt.plan.gscratch["sib"]
+            L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix, tmp, tmp + 4 * c, coef, rt.st)
+            for m, off in zip(self.members, self.offs):
+                for src, pi in ((tmp, m.pg), (tmp + 4 * c, m.pb)):
+                    d = rt.pgrad(pi)
+                    if d is not None:
+                        L.call("yms_copy", d, src + 4 * off, 4 * m.c, rt.st)
+        dz = z                   # dz overwrites z in place
+        L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+               base + self.sh, base + self.mi, coef, self.act, dz, self.zld, 0, None, 0, 0, 0, rt.st)
+        if x.buf.needs_grad:
+            L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                   self.acc_x, rt.st)
+        dw = self._adjacent(rt, "pw")
+        if dw is not None:
+            L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, 0,
+                   rt.gbase + rt.plan.gscratch["wgrad"], self.wg_ws, dw, 0, rt.wst())
+            return
+        for m, off in zip(self.members, self.offs):
+            d = rt.pgrad(m.pw)
+            if d is not None:
+                L.call("yms_conv_wgrad", m.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, off,
+                       rt.gbase + rt.plan.gscratch["wgrad"], m.wg_ws, d, 0, rt.wst())
+
+    def grad_params(self):
+        # member-major within each kind: the flat arena then holds [dbeta_a | dbeta_b],
+        # [dgamma_a | dgamma_b] and [dw_a | dw_b] contiguously (_adjacent)
+        return [m.pb for m in self.members] + [m.pg for m in self.members] + [m.pw for m in self.members]
+
+
 class BiasConvOp:
     """Plain nn.Conv2d with bias (the head's final 1x1 layers, yolov8_head.py:86-109)."""
 
@@ -681,6 +838,26 @@ class Builder:
             self.ops.append(ConvOp(self, mod, x, out, res, act))
         return out
 
+    def sibling_convs(self, mods, x):
+        """Two Conv blocks reading the same input x -> their output views, the channel slots of one
+        buffer (SiblingConvOp), or two separate ConvOps when they cannot share one (different
+        geometry or activation, a first member whose width is not a multiple of 8, or
+        YMS_HEAD_FUSE=0)."""
+        ks = {(m.conv.kernel_size, m.conv.stride, m.conv.padding, m.conv.groups, m.conv.dilation,
+               isinstance(m.activation, torch.nn.SiLU)) for m in mods}
+        fuse = (len(mods) == 2 and len(ks) == 1 and mods[0].conv.groups == 1 and mods[0].conv.out_channels % 8 == 0
+                and os.environ.get("YMS_HEAD_FUSE", "1") != "0")
+        if not fuse:
+            return [m.emit(self, x) for m in mods]
+        conv = mods[0].conv
+        k, s, p = conv.kernel_size[0], conv.stride[0], conv.padding[0]
+        ho, wo = (x.h + 2 * p - k) // s + 1, (x.w + 2 * p - k) // s + 1
+        y = self.new(ho, wo, sum(m.conv.out_channels for m in mods))
+        act = L.ACT_SILU if isinstance(mods[0].activation, torch.nn.SiLU) else L.ACT_NONE
+        op = SiblingConvOp(self, mods, x, y, act)
+        self.ops.append(op)
+        return [m.y for m in op.members]
+
     def add(self, a, b, out=None):
         """y = a + b (b may be None: a placement copy) -> view."""
         if b is not None and (a.h, a.w, a.c) != (b.h, b.w, b.c):
@@ -729,7 +906,7 @@ class Plan:
         # grad arena: activation grads share the activation layout, then backward scratch
         Lg = Layout()
         Lg.size = self.act_bytes
-        self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf", "stemwg")}
+        self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf", "stemwg", "sib")}
         self.gscratch["cnt"] = Lg.alloc(16 * max(self.n_counters, 1))
         self.garena_bytes = Lg.size
         self.eval_bytes = Le.size
@@ -795,10 +972,10 @@ class Plan:
         """(Re)pack weights and fold BN when any parameter / buffer changed."""
         sig = []
         for op in self.ops:
-            if isinstance(op, ConvOp):
-                m = op.mod
-                for t in (m.conv.weight, m.bn.weight, m.bn.bias, m.bn.running_mean, m.bn.running_var):
-                    sig.append((t.data_ptr(), t._version))
+            if isinstance(op, (ConvOp, SiblingConvOp)):
+                for m in (op.bn_modules() if isinstance(op, SiblingConvOp) else (op.mod,)):
+                    for t in (m.conv.weight, m.bn.weight, m.bn.bias, m.bn.running_mean, m.bn.running_var):
+                        sig.append((t.data_ptr(), t._version))
             elif isinstance(op, BiasConvOp):
                 sig.append((op.conv.weight.data_ptr(), op.conv.weight._version))
         sig = tuple(sig)
@@ -818,14 +995,19 @@ class Plan:
         """The batched pack's device job table (built and uploaded on the CURRENT stream on a
         cache miss: call it before handing prepack to another stream)."""
         specs = [sp for op in self.ops if hasattr(op, "pack_specs") for sp in op.pack_specs()]
-        key = tuple((w, dst) for _, w, dst, _ in specs)
+        key = tuple((sp[1], sp[2], sp[4] if len(sp) > 4 else None) for sp in specs)
         cache = self.__dict__.setdefault("_pack_tables", {})
         ent = cache.get(key)
         if ent is None:
             jobs, singles = [], []
-            for sp, w, dst, fd in specs:
+            for spec in specs:
+                sp, w, dst, fd = spec[:4]
                 j = L.PackJob()
                 st = L.lib().yms_pack_job_init(sp, w, dst, fd, ctypes.byref(j))
+                if len(spec) > 4:                 # two sources (SiblingConvOp): batched only
+                    if st != 0:
+                        raise RuntimeError("yms: a two-source weight pack must be batchable")
+                    j.w2, j.split = spec[4]
                 if st == 0:
                     jobs.append(j)
                 else:

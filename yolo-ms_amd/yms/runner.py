@@ -319,8 +319,9 @@ def _bump_bn_counters(plan):
     """nn.BatchNorm2d increments num_batches_tracked in training forward."""
     ts = getattr(plan, "_nbt", None)
     if ts is None:
-        from .plan import ConvOp
-        ts = [op.mod.bn.num_batches_tracked for op in plan.ops if isinstance(op, ConvOp)]
+        from .plan import ConvOp, SiblingConvOp
+        ts = [m.bn.num_batches_tracked for op in plan.ops
+              for m in (op.bn_modules() if isinstance(op, SiblingConvOp) else (op.mod,) if isinstance(op, ConvOp) else ())]
         plan._nbt = ts
     if ts:
         with torch.no_grad():

@@ -47,8 +47,11 @@ class Head(_YmsModule):
         outs = []
         for i, x in enumerate((x0, x1, x2)):
             o = b.new(x.h, x.w, self.no, name=f"head_out{i}")
-            for br, off, c in ((self.box[i], 0, self.coordinates), (self.cls[i], self.coordinates, self.num_classes)):
-                t = br[0].emit(b, x)
+            # the two branches' first convs read the same x_i: one SiblingConvOp (one buffer
+            # [box | cls], one BN backward pass, one input and one weight gradient for both)
+            firsts = b.sibling_convs([self.box[i][0], self.cls[i][0]], x)
+            for br, t, off, c in ((self.box[i], firsts[0], 0, self.coordinates),
+                                  (self.cls[i], firsts[1], self.coordinates, self.num_classes)):
                 t = br[1].emit(b, t)
                 b.conv2d_bias(br[2], t, out=o.slot(off, c))
             outs.append(o)
