@@ -115,6 +115,7 @@ class GradTracker:
     def __init__(self):
         self.written = {}
         self.zero = set()
+        self.writes = None       # buffers any op writes a gradient into (recorded after the seeds)
 
     def _iv(self, v):
         return v.off, v.off + v.c
@@ -163,6 +164,8 @@ class GradTracker:
 
     def write(self, v):
         """-> accumulate flag (0 = first writer, plain store)."""
+        if self.writes is not None:
+            self.writes.add(v.buf.idx)
         if v.buf.zero:                       # padded channels must stay zero: zero whole buffer
             if v.buf.idx not in self.zero:
                 self._zero_buf(v)
@@ -191,12 +194,14 @@ class Rt:
         self._ev = None          # wst(): main -> side ordering event
         self.main = None         # backward: torch stream objects (main, weight-gradient side stream)
         self.side = None
+        self.gover = None        # backward: buffer idx -> incoming output-gradient tensor used in place
 
     def a(self, v):
         return self.base + v.buf.off
 
     def g(self, v):
-        return self.gbase + v.buf.off
+        o = self.gover.get(v.buf.idx) if self.gover else None
+        return o if o is not None else self.gbase + v.buf.off
 
     def cnt(self, i):
         """Arrival counter i of the in-launch BN-backward finalize (zeroed at backward start)."""
@@ -914,12 +919,16 @@ class Plan:
         if self.training:
             T = GradTracker()
             self.seed_acc = [T.write(v) for v in self.outputs]
+            T.writes = set()
             for op in reversed(self.ops):
                 op.plan_grads(T)
                 y = getattr(op, "y", None)
                 if isinstance(y, View) and not any(y is o for o in self.outputs):
                     _check_not_in_place(op, y)
                     T.release(y)
+            # output buffers whose gradient no op writes (only reads): the incoming gradient tensor
+            # can serve as that buffer's gradient in place (runner._seed_grad), no copy
+            self.grad_read_only = {v.buf.idx for v in self.outputs if v.buf.idx not in T.writes}
             self.gzero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.idx in T.zero]
             self.gzero_ranges.append((self.gscratch["cnt"], 16 * max(self.n_counters, 1)))
         self.flops = sum(op.flops for op in self.ops)
