@@ -5,8 +5,8 @@ pass, one input gradient and one weight gradient over both.  Checked against the
 running buffers are bit-identical (each member's conv, statistics and finalize are unchanged; the
 affine pass is elementwise), and the parameter gradients agree to the accumulation-order rounding
 (fp32: the reduce's per-block pixel order differs with the channel count; 16-bit: the unfused
-input gradient rounds dx twice, store then accumulate; checked through the drift from fp32).  The fused fp32 path is also covered by
-every fp32 oracle / golden model test, which run it by default."""
+input gradient rounds dx twice, store then accumulate; checked through the drift from fp32).  The
+fused fp32 path is also covered by every fp32 oracle / golden model test, which run it by default."""
 import pytest
 import torch
 
@@ -61,6 +61,11 @@ def test_sibling_head_convs_match_unfused(version, nc, size, monkeypatch):
         assert torch.equal(a, b)
     for k in b0:
         assert torch.equal(b1[k], b0[k]), k
+    # (nc = 3: the z buffers' padding channels start zeroed -- arena garbage there used to turn the
+    # input gradient NaN through zero weight rows, fused or not)
+    for gg in (g1, g0):
+        bad = [k for k, t in gg.items() if not torch.isfinite(t).all()]
+        assert not bad, bad[:5]
     d1 = torch.tensor([((g1[k] - g32[k]).norm() / (g32[k].norm() + 1e-30)).item() for k in g32])
     d0 = torch.tensor([((g0[k] - g32[k]).norm() / (g32[k].norm() + 1e-30)).item() for k in g32])
     assert d1.median() <= 1.2 * d0.median() and d1.max() <= 1.5 * d0.max(), (d1.median(), d0.median(), d1.max(), d0.max())

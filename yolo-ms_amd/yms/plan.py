@@ -916,6 +916,15 @@ class Plan:
         self.garena_bytes = Lg.size
         self.eval_bytes = Le.size
         self.zero_ranges = [(bf.off, bf.npix * bf.ld * self.es) for bf in self.bufs if bf.zero]
+        # training z buffers with padding channels (c % 8 != 0, e.g. a head with nc = 3): the convs and
+        # the BN apply (dz written over z) touch only the c real channels, while the input gradient
+        # reads the whole 16-B groups -- padding left as arena garbage (NaN / Inf bit patterns) times
+        # the zero weight rows is NaN, so those z buffers start zeroed and their padding stays zero
+        if self.training:
+            for op in self.ops:
+                zld, z = getattr(op, "zld", None), getattr(op, "z", None)
+                if zld is not None and z is not None and zld != op.c:
+                    self.zero_ranges.append((z, op.npix * zld * self.es))
         if self.training:
             T = GradTracker()
             self.seed_acc = [T.write(v) for v in self.outputs]
