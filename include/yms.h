@@ -130,6 +130,20 @@ yms_status yms_conv_stem_wgrad(const yms_conv_shape* s, const float* x, const vo
 yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
                           const void* wpacked_t, void* dx, int dx_ld, int dx_off,
                           int accumulate, void* stream);
+/* Input gradient with the PRODUCER's BN + act backward reduce fused into its epilogue: the producer
+ * (components.py:69-77 Conv before this one) wrote this conv's input x as act(BN(z)), and this dgrad
+ * is the last writer of dx = that producer's output gradient.  dx is stored / accumulated as by
+ * yms_conv_dgrad; from the FINAL dx values (as stored) each persistent block writes one partial row
+ * ws[r][2][cin] = (sum da, sum da * xhat), da = dx * act'(z*scale + shift), xhat = (z - mean)*invstd
+ * (z: view of the dx pixels; scale / shift / mean_invstd as yms_bn_act_bwd_reduce), which replaces
+ * the yms_bn_act_bwd_reduce pass: yms_bn_act_bwd_finalize(cin, ws, rows = yms_conv_dgrad_bnred_rows(s), ..).
+ * Supported where yms_conv_dgrad_bnred_rows(s) > 0 (the direct 3x3 input-gradient kernel's shapes:
+ * 16-bit, 3x3, pad 1, stride 1 or 2, 32 / 64 reduction channels, cin <= 64 and a multiple of 8). */
+int yms_conv_dgrad_bnred_rows(const yms_conv_shape* s);
+yms_status yms_conv_dgrad_bnred(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
+                                const void* wpacked_t, void* dx, int dx_ld, int dx_off, int accumulate,
+                                const void* z, int z_ld, int z_off, const float* scale, const float* shift,
+                                const float* mean_invstd, int act, float* ws, void* stream);
 /* dw[cout][cin][k][k] (+)= sum_pixels x (*) dz, fp32; ws = split-K partial slabs. */
 size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s);
 yms_status yms_conv_wgrad(const yms_conv_shape* s, const void* x, int x_ld, int x_off,

@@ -53,7 +53,92 @@ struct DirectParams {
   int nkt;                     // packed weight k-tiles per row (row pitch nkt * 128 B)
   int wrows;                   // packed weight rows (128-padded): the stride-2 class blocks' pitch
   uint32_t src_bytes, dst_bytes, res_bytes;
+  // input gradient with the producer's BN + act backward reduce fused (BNR): the producer's pre-BN
+  // z (a view of the dx pixels' channels), its scale / shift / [mean | invstd] and act; partial rows
+  // bws[block][2][Ncols] = (sum da, sum da * xhat) over the block's final dx values
+  const char* bz;
+  int bz_ld, bz_off;
+  uint32_t bz_bytes;
+  const float* bsc;
+  const float* bsh;
+  const float* bmi;
+  int bact;
+  float* bws;
 };
+
+// BN + act backward partial sums (bn_pool.hip bn_bwd_reduce_kernel's formula) of one 16-B chunk of
+// the FINAL input gradient g (channels c0 .. c0 + 7, the values as stored) against the producer's z:
+// da = g * act'(z * scale + shift), xhat = (z - mean) * invstd; s1 += da, s2 += da * xhat.
+// bnp: [4][COP] floats in LDS (scale, shift, mean, invstd).
+template <typename T>
+__device__ __forceinline__ void cd_bnred(const float (&g)[8], const u32x4& zraw, const float* bnp, int cop, int c0,
+                                         int act, float* s1, float* s2) {
+  float zv[8];
+  unpack8(*reinterpret_cast<const Raw8<T>*>(&zraw), zv);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float4 sc = *reinterpret_cast<const float4*>(bnp + c0 + 4 * h);
+    const float4 sh = *reinterpret_cast<const float4*>(bnp + cop + c0 + 4 * h);
+    const float4 mu = *reinterpret_cast<const float4*>(bnp + 2 * cop + c0 + 4 * h);
+    const float4 is = *reinterpret_cast<const float4*>(bnp + 3 * cop + c0 + 4 * h);
+    const float scv[4] = {sc.x, sc.y, sc.z, sc.w}, shv[4] = {sh.x, sh.y, sh.z, sh.w};
+    const float muv[4] = {mu.x, mu.y, mu.z, mu.w}, isv[4] = {is.x, is.y, is.z, is.w};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int i = 4 * h + j;
+      float da = g[i];
+      if (act == YMS_ACT_SILU) da = g[i] * dsilu_f(zv[i] * scv[j] + shv[j]);
+      s1[i] += da;
+      s2[i] += da * ((zv[i] - muv[j]) * isv[j]);
+    }
+  }
+}
+
+// Block merge of the per-lane BN-reduce sums: lane (wave, lr, lh) holds channels cf*32 + 16pp + 8lh +
+// (0..7) of its pixels; the 256 lanes of each channel (8 waves x 32) are summed in a fixed order
+// through LDS (scratch: 2 x 16 x 256 floats) and written as row `row` of bws ([rows][2][Ncols]).
+template <int NCF>
+__device__ __forceinline__ void cd_bnred_store(float (&s1)[NCF][16], float (&s2)[NCF][16], char* scratch,
+                                               float* bws, int row, int ncols) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
+  float* const t = reinterpret_cast<float*>(scratch);     // [2][16][256]
+  const int u = tid >> 5, k = tid & 31;                    // thread: channel u of the pass, lane group k
+#pragma unroll
+  for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      if (lh == h) {
+        const int j = wave * 32 + lr;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          t[i * 256 + j] = s1[cf][i];
+          t[(16 + i) * 256 + j] = s2[cf][i];
+        }
+      }
+      __syncthreads();
+      float a = 0.f, b = 0.f;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a += t[u * 256 + 8 * k + e];
+        b += t[(16 + u) * 256 + 8 * k + e];
+      }
+#pragma unroll
+      for (int o = 1; o < 32; o <<= 1) {
+        a += __shfl_xor(a, o);
+        b += __shfl_xor(b, o);
+      }
+      if (k == 0) {                                        // register u = 8pp + jj: channel 16pp + 8h + jj
+
+        const int pp = u >> 3, jj = u & 7;
+        const int c = cf * 32 + 16 * pp + 8 * h + jj;
+        if (c < ncols) {
+          bws[(long)row * 2 * ncols + c] = a;
+          bws[(long)row * 2 * ncols + ncols + c] = b;
+        }
+      }
+      __syncthreads();
+    }
+}
 
 template <int TW, int CP, int NCF> struct DirGeo {
   static constexpr int NTHR = 512, NW = 8, BM = 256, TH = BM / TW;
@@ -65,7 +150,7 @@ template <int TW, int CP, int NCF> struct DirGeo {
   static constexpr int NKT = (9 * CP + 7) / 8;               // packed k-tiles (8 chunks each)
   static constexpr int WBYTES = NKT * COP * 128;
   static constexpr int BUF = HP * PITCH;
-  static constexpr int LDS = WBYTES + 2 * BUF + 2 * COP * 4; // + affine [2][COP]
+  static constexpr int LDS = WBYTES + 2 * BUF + 4 * COP * 4; // + affine [2][COP] / BN-reduce [4][COP]
   static constexpr int OCC = LDS <= 80 * 1024 ? 2 : 1;       // resident blocks per CU
   static constexpr int SS = CP == 8 ? 1 : 2;                 // halo swizzle: chunk ^ ((p >> SS) & (CP-1))
   static constexpr int NST = 2 * NCF;                        // 16-B stores (and operand loads) per lane per tile
@@ -124,8 +209,9 @@ __device__ __forceinline__ void cd_chan(float& n, float& m, float& q, float nb, 
 // wave's epilogue (VALU, stores) overlaps the other waves' MFMAs of the next tile.  BN statistics are
 // per-lane Welford moments over the block's tiles (each lane sees one pixel per tile), merged across
 // lanes and waves (Chan) once at the end.
-template <typename T, int TW, int CP, int NCF, int MODE, int EPI>
+template <typename T, int TW, int CP, int NCF, int MODE, int EPI, bool BNR = false>
 __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_direct_kernel(DirectParams p) {
+  static_assert(!BNR || MODE == MODE_DGRAD, "the BN-reduce epilogue belongs to the input gradient");
   using G = DirGeo<TW, CP, NCF>;
   constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
   constexpr int ES = (int)sizeof(T);
@@ -143,6 +229,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
   const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)p.src_bytes, NT_RSRC3);
   const __amdgpu_buffer_rsrc_t rs_dst = __builtin_amdgcn_make_buffer_rsrc((void*)p.dst, (short)0, (int)p.dst_bytes, NT_RSRC3);
   const __amdgpu_buffer_rsrc_t rs_res = __builtin_amdgcn_make_buffer_rsrc((void*)p.res, (short)0, (int)p.res_bytes, NT_RSRC3);
+  const __amdgpu_buffer_rsrc_t rs_bz = __builtin_amdgcn_make_buffer_rsrc((void*)p.bz, (short)0, (int)p.bz_bytes, NT_RSRC3);
 
   // ---- resident weights: [kt][COP rows][128 B], chunk c of row r at slot c ^ ((r >> 1) & 7) ----
   {
@@ -163,6 +250,16 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
       const bool cv = tid < p.Ncols;
       prm[tid] = (cv && p.scale) ? p.scale[tid] : 1.0f;
       prm[COP + tid] = (cv && p.shift) ? p.shift[tid] : 0.0f;
+    }
+  }
+  if constexpr (BNR) {
+    // the producer's BN parameters [scale | shift | mean | invstd] of the dx channels
+    if (tid < COP) {
+      const bool cv = tid < p.Ncols;
+      prm[tid] = cv ? p.bsc[tid] : 0.0f;
+      prm[COP + tid] = cv ? p.bsh[tid] : 0.0f;
+      prm[2 * COP + tid] = cv ? p.bmi[tid] : 0.0f;
+      prm[3 * COP + tid] = cv ? p.bmi[p.Ncols + tid] : 0.0f;
     }
   }
 
@@ -231,8 +328,20 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
     }
 
   const int my_tiles = (p.ntiles - lb + Gn - 1) / Gn;
-  const bool has_ops = (EPI == EPI_AFFINE && p.res != nullptr) || EPI == EPI_ACCUM;
+  const bool has_rv = (EPI == EPI_AFFINE && p.res != nullptr) || EPI == EPI_ACCUM;
+  const bool has_ops = has_rv || BNR;
   u32x4 rv[NCF][2];      // residual / accumulate operands of the next epilogue
+  u32x4 zv[BNR ? NCF : 1][2];   // BNR: the producer's z at the next epilogue's dx chunks
+  float bs1[BNR ? NCF : 1][16], bs2[BNR ? NCF : 1][16];   // BNR: per-lane sums of da, da * xhat
+  if constexpr (BNR) {
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        bs1[cf][i] = 0.f;
+        bs2[cf][i] = 0.f;
+      }
+  }
   auto load_ops = [&](int t) {
     if (!has_ops) return;
     int n, tyi, txi;
@@ -242,9 +351,15 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp) {
         bool ok;
-        const uint32_t o = EPI == EPI_ACCUM ? out_off(n, tyi, txi, cf, pp, p.dst_ld, p.dst_off, ok)
-                                            : out_off(n, tyi, txi, cf, pp, p.res_ld, p.res_off, ok);
-        rv[cf][pp] = cd_ld16(EPI == EPI_ACCUM ? rs_dst : rs_res, ok ? o : NT_OOB);
+        if (has_rv) {
+          const uint32_t o = EPI == EPI_ACCUM ? out_off(n, tyi, txi, cf, pp, p.dst_ld, p.dst_off, ok)
+                                              : out_off(n, tyi, txi, cf, pp, p.res_ld, p.res_off, ok);
+          rv[cf][pp] = cd_ld16(EPI == EPI_ACCUM ? rs_dst : rs_res, ok ? o : NT_OOB);
+        }
+        if constexpr (BNR) {
+          const uint32_t o = out_off(n, tyi, txi, cf, pp, p.bz_ld, p.bz_off, ok);
+          zv[cf][pp] = cd_ld16(rs_bz, ok ? o : NT_OOB);
+        }
       }
   };
 
@@ -341,7 +456,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
         cd_swap(a0, b0);
         cd_swap(a1, b1);
         u32x4 ov = {a0, a1, b0, b1};     // channels cf*32 + 16pp + 8lh + (0..7)
-        if (has_ops) {
+        if (has_rv) {
           float f[8], r[8];
           unpack8(*reinterpret_cast<const Raw8<T>*>(&ov), f);
           unpack8(*reinterpret_cast<const Raw8<T>*>(&rv[cf][pp]), r);
@@ -351,6 +466,14 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
         bool ok;
         const uint32_t off = out_off(n, tyi, txi, cf, pp, p.dst_ld, p.dst_off, ok);
         cd_st16(rs_dst, ok ? off : NT_OOB, ov);
+        if constexpr (BNR) {
+          if (ok) {     // the stored (rounded) gradient, as the separate reduce pass would read it
+            float g[8];
+            unpack8(*reinterpret_cast<const Raw8<T>*>(&ov), g);
+            cd_bnred<T>(g, zv[cf][pp], prm, COP, cf * 32 + 16 * pp + 8 * lh, p.bact, &bs1[cf][8 * pp],
+                        &bs2[cf][8 * pp]);
+          }
+        }
       }
     }
   };
@@ -372,8 +495,9 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
     const bool has_next = it + 1 < my_tiles;
     if (it > 0) {
       // this wave's halo(t) DMAs have landed: younger are the last epilogue's stores and the next
-      // epilogue's operand loads
-      if (has_ops) wait_vmcnt<2 * G::NST>();
+      // epilogue's operand loads (residual / accumulate operand, BNR: the producer's z)
+      if (has_rv && BNR) wait_vmcnt<3 * G::NST>();
+      else if (has_ops) wait_vmcnt<2 * G::NST>();
       else wait_vmcnt<G::NST>();
       __builtin_amdgcn_s_waitcnt((0xF) | (3 << 14) | (0x7 << 4) | (0 << 8));   // lgkmcnt(0)
       raw_barrier();     // halo(t) visible everywhere; every wave is done reading buffer b ^ 1
@@ -388,6 +512,10 @@ __global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_dire
     if (has_next) load_ops(t + Gn);
   }
 
+  if constexpr (BNR) {
+    __syncthreads();                                    // weights and halo buffers are free now
+    cd_bnred_store<NCF>(bs1, bs2, smem, p.bws, lb, p.Ncols);
+  }
   if constexpr (EPI == EPI_STATS) {
     // Merge the 256 per-lane moment sets of each channel (8 waves x 32 lanes of one half) in LDS,
     // 16 channels (one fragment half) per pass, all 512 threads: thread (u, k) sums contributors
@@ -463,14 +591,14 @@ template <int TW, int CP, int NCF> struct DirGeo2 {
   static constexpr int NKT = cumk(4);
   static constexpr int WBYTES = NKT * COP * 128;
   static constexpr int BUF = HP * PITCH;
-  static constexpr int LDS = WBYTES + 2 * BUF;
+  static constexpr int LDS = WBYTES + 2 * BUF + 4 * COP * 4;   // + BN-reduce parameters [4][COP]
   static constexpr int OCC = LDS <= 80 * 1024 ? 2 : 1;
   static constexpr int SS = CP == 8 ? 1 : 2;
   static constexpr int NST = 2 * NCF;                  // 16-B stores per lane per class
   static_assert((CP == 4 || CP == 8) && BM % TW == 0 && LDS <= 160 * 1024, "tile");
 };
 
-template <typename T, int TW, int CP, int NCF, int EPI>
+template <typename T, int TW, int CP, int NCF, int EPI, bool BNR = false>
 __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_direct_dgrad2_kernel(DirectParams p) {
   using G = DirGeo2<TW, CP, NCF>;
   constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
@@ -478,6 +606,7 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
   extern __shared__ __attribute__((aligned(16))) char smem[];
   char* const wts = smem;
   char* const bufs = smem + G::WBYTES;
+  float* const bnp = reinterpret_cast<float*>(smem + G::WBYTES + 2 * BUF);   // BNR: [4][COP]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, lr = lane & 31, lh = lane >> 5;
   const int wv = __builtin_amdgcn_readfirstlane(wave);
@@ -487,6 +616,16 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
 
   const __amdgpu_buffer_rsrc_t rs_src = __builtin_amdgcn_make_buffer_rsrc((void*)p.src, (short)0, (int)p.src_bytes, NT_RSRC3);
   const __amdgpu_buffer_rsrc_t rs_dst = __builtin_amdgcn_make_buffer_rsrc((void*)p.dst, (short)0, (int)p.dst_bytes, NT_RSRC3);
+  const __amdgpu_buffer_rsrc_t rs_bz = __builtin_amdgcn_make_buffer_rsrc((void*)p.bz, (short)0, (int)p.bz_bytes, NT_RSRC3);
+  if constexpr (BNR) {
+    if (tid < COP) {
+      const bool cv = tid < p.Ncols;
+      bnp[tid] = cv ? p.bsc[tid] : 0.0f;
+      bnp[COP + tid] = cv ? p.bsh[tid] : 0.0f;
+      bnp[2 * COP + tid] = cv ? p.bmi[tid] : 0.0f;
+      bnp[3 * COP + tid] = cv ? p.bmi[p.Ncols + tid] : 0.0f;
+    }
+  }
 
   // ---- resident weights: class blocks [kt][COP][128 B] (swizzled as in the stride-1 kernel) ----
   {
@@ -541,11 +680,11 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
   const int hr = wave * 32 + lr;
   const int oty = hr / TW, otx = hr - (hr / TW) * TW;
   // dx pixel (2a + ry, 2b + rx) of this lane's position, chunk (cf, pp)
-  auto out_off = [&](int n, int tyi, int txi, int cls, int cf, int pp, bool& ok) -> uint32_t {
+  auto out_off = [&](int n, int tyi, int txi, int cls, int cf, int pp, bool& ok, int ld, int off) -> uint32_t {
     const int oy = 2 * (tyi * TH + oty) + (cls >> 1), ox = 2 * (txi * TW + otx) + (cls & 1);
     const int c0 = cf * 32 + 16 * pp + 8 * lh;
     ok = oy < p.OH && ox < p.OW && c0 < p.Ncols;
-    return (uint32_t)((((n * p.OH + oy) * p.OW + ox) * p.dst_ld + p.dst_off + c0) * ES);
+    return (uint32_t)((((n * p.OH + oy) * p.OW + ox) * ld + off + c0) * ES);
   };
   int bb[NCF];
 #pragma unroll
@@ -556,9 +695,20 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
 
   const int my_tiles = (p.ntiles - lb + Gn - 1) / Gn;
   constexpr bool ACC = EPI == EPI_ACCUM;
-  u32x4 rv[4][NCF][2];
+  u32x4 rv[ACC ? 4 : 1][NCF][2];
+  u32x4 zv[BNR ? 4 : 1][NCF][2];   // BNR: the producer's z at the next tile's dx chunks
+  float bs1[BNR ? NCF : 1][16], bs2[BNR ? NCF : 1][16];
+  if constexpr (BNR) {
+#pragma unroll
+    for (int cf = 0; cf < NCF; ++cf)
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        bs1[cf][i] = 0.f;
+        bs2[cf][i] = 0.f;
+      }
+  }
   auto load_ops = [&](int t) {
-    if constexpr (!ACC) return;
+    if constexpr (!ACC && !BNR) return;
     int n, tyi, txi;
     tile_pos(t, n, tyi, txi);
 #pragma unroll
@@ -568,8 +718,14 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
 #pragma unroll
         for (int pp = 0; pp < 2; ++pp) {
           bool ok;
-          const uint32_t o = out_off(n, tyi, txi, c, cf, pp, ok);
-          rv[c][cf][pp] = cd_ld16(rs_dst, ok ? o : NT_OOB);
+          if constexpr (ACC) {
+            const uint32_t o = out_off(n, tyi, txi, c, cf, pp, ok, p.dst_ld, p.dst_off);
+            rv[c][cf][pp] = cd_ld16(rs_dst, ok ? o : NT_OOB);
+          }
+          if constexpr (BNR) {
+            const uint32_t o = out_off(n, tyi, txi, c, cf, pp, ok, p.bz_ld, p.bz_off);
+            zv[c][cf][pp] = cd_ld16(rs_bz, ok ? o : NT_OOB);
+          }
         }
   };
 
@@ -633,8 +789,16 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
                      cd_pack2<T>(f[4] + r[4], f[5] + r[5]), cd_pack2<T>(f[6] + r[6], f[7] + r[7])};
         }
         bool ok;
-        const uint32_t off = out_off(n, tyi, txi, c, cf, pp, ok);
+        const uint32_t off = out_off(n, tyi, txi, c, cf, pp, ok, p.dst_ld, p.dst_off);
         cd_st16(rs_dst, ok ? off : NT_OOB, ov);
+        if constexpr (BNR) {
+          if (ok) {
+            float g[8];
+            unpack8(*reinterpret_cast<const Raw8<T>*>(&ov), g);
+            cd_bnred<T>(g, zv[c][cf][pp], bnp, COP, cf * 32 + 16 * pp + 8 * lh, p.bact, &bs1[cf][8 * pp],
+                        &bs2[cf][8 * pp]);
+          }
+        }
       }
   };
 
@@ -649,14 +813,14 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
     const int b = it & 1;
     const bool has_next = it + 1 < my_tiles;
     if (it > 0) {
-      if (ACC) wait_vmcnt<(ACC ? 8 : 4) * G::NST>();    // younger: 4 classes' stores (+ ops(t))
-      else wait_vmcnt<4 * G::NST>();
+      // younger than halo(t): 4 classes' stores (+ ops(t): accumulate operands, BNR z)
+      wait_vmcnt<(4 + (ACC ? 4 : 0) + (BNR ? 4 : 0)) * G::NST>();
       __builtin_amdgcn_s_waitcnt((0xF) | (3 << 14) | (0x7 << 4) | (0 << 8));   // lgkmcnt(0)
       raw_barrier();
       if (has_next) issue_halo(t + Gn, b ^ 1);
     }
     compute(b, std::integral_constant<int, 0>{});
-    if constexpr (ACC) {
+    if constexpr (ACC || BNR) {
       if (has_next) wait_vmcnt<G::NP - 1>();     // ops(t); halo(t + G) may stay in flight
       else wait_vmcnt<0>();
     }
@@ -668,6 +832,10 @@ __global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_dir
     compute(b, std::integral_constant<int, 3>{});
     epilogue(t, 3);
     if (has_next) load_ops(t + Gn);
+  }
+  if constexpr (BNR) {
+    __syncthreads();
+    cd_bnred_store<NCF>(bs1, bs2, smem, p.bws, lb, p.Ncols);
   }
 }
 
@@ -726,10 +894,10 @@ bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g) {
   return true;
 }
 
-template <typename T, int TW, int CP, int NCF, int MODE, int EPI>
+template <typename T, int TW, int CP, int NCF, int MODE, int EPI, bool BNR = false>
 static void launch_direct(const DirectParams& p, int grid, hipStream_t st) {
   using G = DirGeo<TW, CP, NCF>;
-  auto k = conv_direct_kernel<T, TW, CP, NCF, MODE, EPI>;
+  auto k = conv_direct_kernel<T, TW, CP, NCF, MODE, EPI, BNR>;
   static bool attr = false;
   if (!attr) {
     (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
@@ -743,26 +911,36 @@ static void launch_direct_epi(const DirectParams& p, int mode, int epi, int grid
   if (mode == 0) {
     if (epi == EPI_STATS) launch_direct<T, TW, CP, NCF, MODE_FWD, EPI_STATS>(p, grid, st);
     else launch_direct<T, TW, CP, NCF, MODE_FWD, EPI_AFFINE>(p, grid, st);
+  } else if (p.bws) {
+    if (epi == EPI_ACCUM) launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_ACCUM, true>(p, grid, st);
+    else launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_STORE, true>(p, grid, st);
   } else {
     if (epi == EPI_ACCUM) launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_ACCUM>(p, grid, st);
     else launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_STORE>(p, grid, st);
   }
 }
 
-template <typename T, int TW, int CP, int NCF>
-static void launch_dgrad2(const DirectParams& p, int epi, int grid, hipStream_t st) {
+template <typename T, int TW, int CP, int NCF, int EPI, bool BNR>
+static void launch_dgrad2_k(const DirectParams& p, int grid, hipStream_t st) {
   using G = DirGeo2<TW, CP, NCF>;
-  auto k = epi == EPI_ACCUM ? conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_ACCUM>
-                            : conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_STORE>;
+  auto k = conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI, BNR>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_ACCUM>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
-    (void)hipFuncSetAttribute((const void*)conv_direct_dgrad2_kernel<T, TW, CP, NCF, EPI_STORE>,
-                              hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
+    (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS);
     attr = true;
   }
   hipLaunchKernelGGL(k, dim3((unsigned)grid), dim3(G::NTHR), G::LDS, st, p);
+}
+
+template <typename T, int TW, int CP, int NCF>
+static void launch_dgrad2(const DirectParams& p, int epi, int grid, hipStream_t st) {
+  if (p.bws) {
+    if (epi == EPI_ACCUM) launch_dgrad2_k<T, TW, CP, NCF, EPI_ACCUM, true>(p, grid, st);
+    else launch_dgrad2_k<T, TW, CP, NCF, EPI_STORE, true>(p, grid, st);
+  } else {
+    if (epi == EPI_ACCUM) launch_dgrad2_k<T, TW, CP, NCF, EPI_ACCUM, false>(p, grid, st);
+    else launch_dgrad2_k<T, TW, CP, NCF, EPI_STORE, false>(p, grid, st);
+  }
 }
 
 // (32 reduction channels with 33..64 outputs is not instantiated: at two blocks per CU its four
@@ -814,8 +992,22 @@ static void launch_direct_t(const DirectGeo& g, const DirectParams& p, int mode,
 yms_status conv_direct_launch(const yms_conv_shape* s, int mode, const DirectGeo& g, const void* src, int src_ld,
                               int src_off, const void* wpacked, void* dst, int dst_ld, int dst_off,
                               const float* scale, const float* shift, int act, const void* res, int res_ld,
-                              int res_off, float* stats, int accumulate, hipStream_t st) {
+                              int res_off, float* stats, int accumulate, hipStream_t st, const DirectBnRed* bnr) {
   DirectParams p{};
+  if (bnr) {
+    if (mode != 1 || !bnr->z || !bnr->scale || !bnr->shift || !bnr->mean_invstd || !bnr->ws) return YMS_ERR_INVALID;
+    const long zb = (long)s->n * s->h * s->w * bnr->z_ld * 2;
+    if (zb >= (1l << 31) - (1l << 20)) return YMS_ERR_UNSUPPORTED;
+    p.bz = (const char*)bnr->z;
+    p.bz_ld = bnr->z_ld;
+    p.bz_off = bnr->z_off;
+    p.bz_bytes = (uint32_t)zb;
+    p.bsc = bnr->scale;
+    p.bsh = bnr->shift;
+    p.bmi = bnr->mean_invstd;
+    p.bact = bnr->act;
+    p.bws = bnr->ws;
+  }
   p.src = (const char*)src;
   p.wp = (const char*)wpacked;
   p.dst = (char*)dst;

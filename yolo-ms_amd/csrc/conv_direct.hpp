@@ -22,9 +22,22 @@ struct DirectGeo {
 // Off when YMS_DIRECT=0 at the first call or after yms_conv_direct_set(0) (A/B and tests).
 bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g);
 
+// The producer's BN + act backward reduce fused into an input gradient's epilogue (yms_conv_dgrad_bnred):
+// z view of the dx pixels, its BN scale / shift / [mean | invstd], act, partial rows ws[grid][2][cin].
+struct DirectBnRed {
+  const void* z;
+  int z_ld, z_off;
+  const float* scale;
+  const float* shift;
+  const float* mean_invstd;
+  int act;
+  float* ws;
+};
+
 yms_status conv_direct_launch(const yms_conv_shape* s, int mode, const DirectGeo& g, const void* src, int src_ld,
                               int src_off, const void* wpacked, void* dst, int dst_ld, int dst_off,
                               const float* scale, const float* shift, int act, const void* res, int res_ld,
-                              int res_off, float* stats, int accumulate, hipStream_t st);
+                              int res_off, float* stats, int accumulate, hipStream_t st,
+                              const DirectBnRed* bnr = nullptr);
 
 }  // namespace yms

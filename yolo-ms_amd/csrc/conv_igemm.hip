@@ -1617,6 +1617,28 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
   return dispatch_nt<MODE_DGRAD, EPI_STORE>(p, s->dtype, s->k, tc.cfg, st);
 }
 
+int yms_conv_dgrad_bnred_rows(const yms_conv_shape* s) {
+  DirectGeo dg;
+  if (!shape_ok(s) || s->cin % 8 != 0 || !conv_direct_geometry(s, 1, &dg)) return 0;
+  return dg.grid;
+}
+
+yms_status yms_conv_dgrad_bnred(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
+                                const void* wpacked_t, void* dx, int dx_ld, int dx_off, int accumulate,
+                                const void* z, int z_ld, int z_off, const float* scale, const float* shift,
+                                const float* mean_invstd, int act, float* ws, void* stream) {
+  if (!shape_ok(s) || !dz || !wpacked_t || !dx || !z || !scale || !shift || !mean_invstd || !ws)
+    return YMS_ERR_INVALID;
+  if (!view_ok(dz_ld, dz_off, s->cout) || !view_ok(dx_ld, dx_off, s->cin) || !view_ok(z_ld, z_off, s->cin))
+    return YMS_ERR_INVALID;
+  if (act != YMS_ACT_NONE && act != YMS_ACT_SILU) return YMS_ERR_INVALID;
+  DirectGeo dg;
+  if (s->cin % 8 != 0 || !conv_direct_geometry(s, 1, &dg)) return YMS_ERR_UNSUPPORTED;
+  const DirectBnRed b{z, z_ld, z_off, scale, shift, mean_invstd, act, ws};
+  return conv_direct_launch(s, 1, dg, dz, dz_ld, dz_off, wpacked_t, dx, dx_ld, dx_off, nullptr, nullptr, 0, nullptr,
+                            0, 0, nullptr, accumulate, (hipStream_t)stream, &b);
+}
+
 size_t yms_conv_wgrad_ws_bytes(const yms_conv_shape* s) {
   if (!shape_ok(s)) return 0;
   WHPlan wh;

@@ -69,6 +69,8 @@ _SIGS = {
     "yms_conv_stem_wgrad_ws_bytes": (_SZ, [_SP]),
     "yms_conv_stem_wgrad": (_I, [_SP, _P, _P, _I, _I, _P, _I, _I, _P, _P, _P, _P, _I, _P, _SZ, _P, _I, _P]),
     "yms_conv_dgrad": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _I, _P]),
+    "yms_conv_dgrad_bnred_rows": (_I, [_SP]),
+    "yms_conv_dgrad_bnred": (_I, [_SP, _P, _I, _I, _P, _P, _I, _I, _I, _P, _I, _I, _P, _P, _P, _I, _P, _P]),
     "yms_conv_wgrad_ws_bytes": (_SZ, [_SP]),
     "yms_conv_wgrad": (_I, [_SP, _P, _I, _I, _P, _I, _I, _P, _SZ, _P, _I, _P]),
     "yms_bn_fold": (_I, [_I, _P, _P, _P, _P, _F, _P, _P, _P]),
@@ -146,7 +148,7 @@ def check(status, what):
 
 
 _prof = None
-_CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_wgrad", "yms_conv_stem_fwd")
+_CONV = ("yms_conv_fwd", "yms_conv_dgrad", "yms_conv_dgrad_bnred", "yms_conv_wgrad", "yms_conv_stem_fwd")
 _DW = ("yms_dwconv_fwd", "yms_dwconv_dgrad", "yms_dwconv_wgrad")
 # launches whose hipStream_t is the last argument (status-returning entry points ending in a void*)
 # (host-only entry points whose last pointer is a host buffer are listed out explicitly)
@@ -171,6 +173,8 @@ def _work(name, args):
         fl = 2 * sh.n * sh.ho * sh.wo * sh.cout * sh.cin * sh.k * sh.k
         es = _elt(sh.dtype)
         act = (sh.n * sh.h * sh.w * sh.cin + sh.n * sh.ho * sh.wo * sh.cout) * es
+        if name == "yms_conv_dgrad_bnred":             # + the producer's z at the dx pixels
+            act += sh.n * sh.h * sh.w * sh.cin * es
         return fl, act + sh.cout * sh.cin * sh.k * sh.k * (4 if name == "yms_conv_wgrad" else es)
     if name in _DW:
         d = args[0].contents

@@ -245,6 +245,9 @@ class ConvOp:
         self.pb = b.param(mod.bn, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
+        self.bnred_for = None    # producer whose BN-backward reduce this conv's input gradient computes
+        self.bnred_by = None     # consumer whose input gradient computes this conv's BN-backward reduce
+        self.bnred_key = None    # grad-scratch region of those partial rows
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -341,10 +344,15 @@ class ConvOp:
         ws = rt.gbase + rt.plan.gscratch["bwd"]
         coef = rt.gbase + rt.plan.gscratch["coef"]
         z = base + self.z
-        L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
-               base + self.sh, base + self.mi, self.act, ws, rt.st)
-        L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix,
-               rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        if self.bnred_by is not None:
+            # the consumer's input gradient (its last writer) already summed the partial rows
+            L.call("yms_bn_act_bwd_finalize", c, rt.gbase + rt.plan.gscratch[self.bnred_key], self.bnred_rows,
+                   self.npix, rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
+        else:
+            L.call("yms_bn_act_bwd_reduce", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
+                   base + self.sh, base + self.mi, self.act, ws, rt.st)
+            L.call("yms_bn_act_bwd_finalize", c, ws, self.bwd_rows, self.npix,
+                   rt.pgrad(self.pg), rt.pgrad(self.pb), coef, rt.st)
         if self.stem_input is not None:
             # the stem's input needs no gradient: the apply pass is fused into the weight
             # gradient, which reads gy, z and the NCHW input.
@@ -367,8 +375,15 @@ class ConvOp:
                base + self.sh, base + self.mi, coef, self.act, dz, self.zld, 0, gres, gro[0], gro[1], self.acc_res,
                rt.st)
         if x.buf.needs_grad:
-            L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
-                   self.acc_x, rt.st)
+            q = self.bnred_for
+            if q is not None:
+                # + the producer's BN-backward reduce in the epilogue (dx = the producer's final gy)
+                L.call("yms_conv_dgrad_bnred", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                       self.acc_x, base + q.z, q.zld, 0, base + q.sc, base + q.sh, base + q.mi, q.act,
+                       rt.gbase + rt.plan.gscratch[self.bnred_key], rt.st)
+            else:
+                L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                       self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             wsz = self.wg_ws
@@ -632,6 +647,8 @@ class DWConvOp(ConvOp):
         self.pb = b.param(mod.bn, "bias")
         self.flops = 0          # not an MFMA contraction: excluded from the conv roofline
         self.dw_flops = 2 * self.npix * c * k * k
+        self.stem_input = None
+        self.bnred_for = self.bnred_by = self.bnred_key = None   # (ConvOp's fused-reduce links: unused)
 
     def layout(self, plan, La, Le):
         es, c = plan.es, self.c
@@ -898,6 +915,7 @@ class Plan:
         self.scratch_req = {}
         self.n_counters = 0
         self.stem_inputs = self._find_stems()
+        self._find_bnred()
         La, Le = Layout(), Layout()
         for buf in self.bufs:
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
@@ -912,6 +930,8 @@ class Plan:
         Lg = Layout()
         Lg.size = self.act_bytes
         self.gscratch = {k: Lg.alloc(self.scratch_req.get(k, 0)) for k in ("bwd", "coef", "wgrad", "sppf", "stemwg", "sib")}
+        for k in sorted(k for k in self.scratch_req if k.startswith("bnr")):
+            self.gscratch[k] = Lg.alloc(self.scratch_req[k])
         self.gscratch["cnt"] = Lg.alloc(16 * max(self.n_counters, 1))
         self.garena_bytes = Lg.size
         self.eval_bytes = Le.size
@@ -973,6 +993,49 @@ class Plan:
                 op.stem_input = i
                 out[i] = op
         return out
+
+    def _find_bnred(self):
+        """Training, 16-bit: a Conv whose input gradient runs on the direct 3x3 kernel
+        (yms_conv_dgrad_bnred_rows > 0) and whose input view is exactly the output of an earlier
+        Conv op P, with no op in between touching that view (so this dgrad is the LAST writer of
+        P's output gradient, backward order), computes P's BN + act backward reduce in its epilogue
+        (yms_conv_dgrad_bnred): P's separate reduce pass (z and gy read once more) goes, and P's
+        finalize reads the partial rows from a grad-scratch region of their own.  YMS_BNRED=0 keeps
+        the separate reduce (A/B)."""
+        if not self.training or self.dt == L.F32 or os.environ.get("YMS_BNRED", "1") == "0":
+            return
+
+        def views(op):
+            for v in vars(op).values():
+                for u in (v if isinstance(v, (list, tuple)) else (v,)):
+                    if isinstance(u, View):
+                        yield u
+
+        n = 0
+        for i, c in enumerate(self.ops):
+            if type(c) is not ConvOp or c.stem_input is not None or not c.x.buf.needs_grad:
+                continue
+            rows = L.lib().yms_conv_dgrad_bnred_rows(c.sp)
+            if rows <= 0:
+                continue
+            x = c.x
+            j = next((j for j in range(i - 1, -1, -1)
+                      if isinstance(getattr(self.ops[j], "y", None), View) and _overlap(self.ops[j].y, x)), None)
+            if j is None:
+                continue
+            q = self.ops[j]
+            if (type(q) is not ConvOp or q.y.off != x.off or q.y.c != x.c or q.c != x.c or q.bnred_by is not None
+                    or q.act not in (L.ACT_NONE, L.ACT_SILU)):
+                continue
+            if any(_overlap(v, x) for op in self.ops[j + 1:i] for v in views(op)):
+                continue
+            if any(_overlap(v, x) for k, v in vars(c).items() if isinstance(v, View) and k != "x"):
+                continue
+            key = f"bnr{n}"
+            n += 1
+            c.bnred_for, c.bnred_key = q, key
+            q.bnred_by, q.bnred_key, q.bnred_rows = c, key, rows
+            self.need_scratch(key, 4 * rows * 2 * r8(x.c))
 
     def counter(self):
         """Reserve one 16-B arrival counter in the grad scratch (-> its index)."""
