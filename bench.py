@@ -112,12 +112,15 @@ def graphed(step, warmup):
 
 def add_traffic(roof, mode, workload):
     t, src, busy = pmc_traffic(mode, workload)
+    roof["traffic_libyms_sha256"] = loaded_lib_sha256()
     if t is not None:
         roof["traffic"] = round(t)
         roof["traffic_unit"] = "bytes below L2 per conv launch (PMC)"
         roof["traffic_source"] = src
         if busy is not None:
             roof["mfma_busy_frac_pmc"] = round(busy, 4)
+    else:
+        roof["traffic_source"] = "none: no PMC profile of this workload with the loaded libyms.so build"
 
 
 def conv_roofline(prof, label):
@@ -225,18 +228,37 @@ class MeanSquare(torch.autograd.Function):
         return o * (g * (2.0 / o.numel())).to(o.dtype)
 
 
+_LIB_SHA = None
+
+
+def loaded_lib_sha256():
+    """sha256 of the libyms.so this process runs (yms._lib.LIB_PATH)."""
+    global _LIB_SHA
+    if _LIB_SHA is None:
+        import hashlib
+        from yms import _lib
+        _LIB_SHA = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+    return _LIB_SHA
+
+
 def pmc_traffic(mode, workload):
-    """HBM bytes per conv call from the newest committed PMC profile of the same workload
-    (profiles/*_pmc_traffic.json, written by tools/profile_round.sh + tools/rocprof_summary.py
-    from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this script).  PMC
-    counters cannot be read from inside the timed run, so this is the profiled value of the
-    same command; None when no profile of this exact workload exists."""
+    """HBM bytes per conv call from the newest committed PMC profile of the same workload AND the
+    same library build (profiles/*_pmc_traffic.json, written by tools/profile_round.sh +
+    tools/rocprof_summary.py from separate rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes of this
+    script, with the sha256 of the libyms.so they profiled).  PMC counters cannot be read from
+    inside the timed run, so this is the profiled value of the same command on the same kernels;
+    None when no profile of this workload was taken with the loaded library (a profile of an
+    older build is never attached: its kernels are not the ones timed)."""
     import glob
+    sha = loaded_lib_sha256()
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_traffic.json")), reverse=True):
         try:
-            d = json.load(open(f)).get(mode, {})
+            j = json.load(open(f))
         except Exception:
             continue
+        if j.get("libyms_sha256") != sha:
+            continue
+        d = j.get(mode, {})
         if d.get("bench_config", {}).get("workload") == workload and "conv_hbm_bytes_per_call" in d:
             return d["conv_hbm_bytes_per_call"], os.path.relpath(f, ROOT), d.get("conv_mfma_busy_frac")
     return None, None, None

@@ -85,9 +85,15 @@ def pmc(paths):
 def traffic(out_dir):
     """profile_round.sh output dir -> {mode: {families, conv_hbm_bytes_per_call, ...}}."""
     import os
+    import hashlib
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    lib = os.environ.get("YMS_LIB") or os.path.join(root, "yolo-ms_amd", "yms", "libyms.so")
     res = {"source": "rocprofv3 --pmc FETCH_SIZE | WRITE_SIZE | SQ_VALU_MFMA_BUSY_CYCLES GRBM_GUI_ACTIVE "
                      "SQ_BUSY_CYCLES, separate passes of `bench.py --mode M --steps 2 --warmup 1`; "
-                     "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 half-counted 128-B reads)"}
+                     "bytes = (2*FETCH_SIZE + WRITE_SIZE)*1024 (gfx950 half-counted 128-B reads)",
+           # the library the passes ran: bench.py attaches this profile's traffic only to runs of
+           # the same build (VERDICT r05: a stale profile must not be reported as current)
+           "libyms_sha256": hashlib.sha256(open(lib, "rb").read()).hexdigest()}
     for mode in ("train", "infer"):
         paths = [os.path.join(out_dir, f"pmc_{mode}_{c}", "run_counter_collection.csv")
                  for c in ("fetch_size", "write_size", "sq_valu_mfma_busy_cycles")]
