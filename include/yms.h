@@ -138,7 +138,7 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
  * (z: view of the dx pixels; scale / shift / mean_invstd as yms_bn_act_bwd_reduce), which replaces
  * the yms_bn_act_bwd_reduce pass: yms_bn_act_bwd_finalize(cin, ws, rows = yms_conv_dgrad_bnred_rows(s), ..).
  * Supported where yms_conv_dgrad_bnred_rows(s) > 0 (the direct 3x3 input-gradient kernel's shapes:
- * 16-bit, 3x3, pad 1, stride 1 or 2, 32 / 64 reduction channels, cin <= 64 and a multiple of 8). */
+ * 16-bit, 3x3, pad 1, stride 1 or 2, 32 / 64 reduction channels, cin <= 32 and a multiple of 8). */
 int yms_conv_dgrad_bnred_rows(const yms_conv_shape* s);
 yms_status yms_conv_dgrad_bnred(const yms_conv_shape* s, const void* dz, int dz_ld, int dz_off,
                                 const void* wpacked_t, void* dx, int dx_ld, int dx_off, int accumulate,

@@ -6,8 +6,8 @@ Against the separate path on the same operands: yms_conv_dgrad (store / accumula
 yms_bn_act_bwd_reduce over (z, dx) and yms_bn_act_bwd_finalize.  dx must be bit-identical (the same
 MFMA sums and rounding); dgamma / dbeta / the apply coefficients agree to fp32 summation order, and
 both match an fp64 evaluation of the reduce formula on the stored dx.  Shapes: the stride-1 kernel
-(tile widths 32 / 16, 32 / 64 reduction channels, 8..64 dx channels, ragged heights, channel slices
-of wider buffers) and the stride-2 parity-class kernel (the stem's 320^2 32 <- 64 layer at reduced
+(tile widths 32 / 16, 32 / 64 reduction channels, 8..32 dx channels, ragged heights, channel slices
+of wider buffers; 33..64 dx channels report 0 rows: two fragments' sums exceed the registers) and the stride-2 parity-class kernel (the stem's 320^2 32 <- 64 layer at reduced
 batch, odd maps)."""
 import ctypes
 
@@ -22,17 +22,17 @@ pytestmark = pytest.mark.gpu
 # (n, cin = dx channels, h, w, cout = reduction channels, stride, accumulate)
 CASES = [
     (2, 32, 32, 64, 32, 1, 0),
-    (2, 64, 40, 32, 64, 1, 0),
-    (2, 64, 40, 32, 64, 1, 1),
+    (2, 32, 40, 32, 64, 1, 0),
+    (2, 32, 40, 32, 64, 1, 1),
     (2, 32, 23, 48, 64, 1, 1),
     (1, 24, 37, 16, 32, 1, 0),
-    (3, 64, 16, 16, 64, 1, 0),
-    (4, 64, 80, 80, 64, 1, 0),
+    (3, 16, 16, 16, 64, 1, 1),
+    (4, 32, 80, 80, 32, 1, 1),
     (2, 32, 160, 160, 32, 1, 0),
     (2, 32, 320, 320, 64, 2, 0),
     (2, 32, 64, 64, 64, 2, 1),
     (1, 32, 33, 63, 64, 2, 0),
-    (2, 64, 30, 64, 64, 2, 0),
+    (2, 8, 30, 64, 32, 2, 0),
 ]
 
 
@@ -106,11 +106,11 @@ def test_dgrad_bnred_f16(case):
 
 def test_dgrad_bnred_rows_and_refusals():
     """Rows = the direct kernel's persistent blocks; shapes outside it (fp32, 128 reduction channels,
-    widths off the tile grid) report 0 rows and the call returns YMS_ERR_UNSUPPORTED."""
-    ok = shape(64, 80, 80, 64, 64, 3, 1, torch.bfloat16)
-    assert 1 <= L.lib().yms_conv_dgrad_bnred_rows(ctypes.pointer(ok)) <= 64 * 5 * 5
-    for bad in (shape(2, 80, 80, 64, 64, 3, 1, torch.float32), shape(2, 40, 40, 64, 128, 3, 1, torch.bfloat16),
-                shape(2, 40, 40, 64, 64, 3, 1, torch.bfloat16)):
+    widths off the tile grid, 64 dx channels) report 0 rows and the call returns YMS_ERR_UNSUPPORTED."""
+    ok = shape(64, 160, 160, 32, 32, 3, 1, torch.bfloat16)
+    assert 1 <= L.lib().yms_conv_dgrad_bnred_rows(ctypes.pointer(ok)) <= 64 * 5 * 20
+    for bad in (shape(2, 80, 80, 32, 64, 3, 1, torch.float32), shape(2, 40, 40, 32, 128, 3, 1, torch.bfloat16),
+                shape(2, 40, 40, 32, 64, 3, 1, torch.bfloat16), shape(2, 80, 80, 64, 64, 3, 1, torch.bfloat16)):
         sp = ctypes.pointer(bad)
         assert L.lib().yms_conv_dgrad_bnred_rows(sp) == 0
         t = torch.zeros(16, device="cuda")

@@ -209,8 +209,10 @@ __device__ __forceinline__ void cd_chan(float& n, float& m, float& q, float nb, 
 // wave's epilogue (VALU, stores) overlaps the other waves' MFMAs of the next tile.  BN statistics are
 // per-lane Welford moments over the block's tiles (each lane sees one pixel per tile), merged across
 // lanes and waves (Chan) once at the end.
+// BNR variants run one block per CU (2 waves per SIMD: up to 256 VGPRs, so the per-lane sums never
+// spill -- scratch traffic would also break the counted vmcnt waits)
 template <typename T, int TW, int CP, int NCF, int MODE, int EPI, bool BNR = false>
-__global__ __launch_bounds__(512, (2 * DirGeo<TW, CP, NCF>::OCC)) void conv_direct_kernel(DirectParams p) {
+__global__ __launch_bounds__(512, (BNR ? 2 : 2 * DirGeo<TW, CP, NCF>::OCC)) void conv_direct_kernel(DirectParams p) {
   static_assert(!BNR || MODE == MODE_DGRAD, "the BN-reduce epilogue belongs to the input gradient");
   using G = DirGeo<TW, CP, NCF>;
   constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
@@ -599,7 +601,7 @@ template <int TW, int CP, int NCF> struct DirGeo2 {
 };
 
 template <typename T, int TW, int CP, int NCF, int EPI, bool BNR = false>
-__global__ __launch_bounds__(512, (2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_direct_dgrad2_kernel(DirectParams p) {
+__global__ __launch_bounds__(512, (BNR ? 2 : 2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_direct_dgrad2_kernel(DirectParams p) {
   using G = DirGeo2<TW, CP, NCF>;
   constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
   constexpr int ES = (int)sizeof(T);
@@ -863,7 +865,7 @@ static int& direct_route() {
   return on;
 }
 
-bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g) {
+bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g, bool bnred) {
   if (!direct_route()) return false;
   if (!s || s->dtype == YMS_F32 || s->k != 3 || s->pad != 1) return false;
   const bool s2 = s->stride == 2;
@@ -888,7 +890,10 @@ bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g) {
   q.tiles_y = cdiv(gh, q.TH);
   q.ntiles = (long)s->n * q.tiles_x * q.tiles_y;
   if (q.ntiles >= (1l << 30)) return false;
-  const int occ = s2 ? direct_occ<DirGeo2>(q.TW, q.CP, q.NCF) : direct_occ<DirGeo>(q.TW, q.CP, q.NCF);
+  // the BN-reduce epilogue: 32-channel output fragments only (two fragments' sums, operands and
+  // fragments exceed 256 VGPRs), one block per CU
+  if (bnred && (mode != 1 || q.NCF != 1)) return false;
+  const int occ = bnred ? 1 : s2 ? direct_occ<DirGeo2>(q.TW, q.CP, q.NCF) : direct_occ<DirGeo>(q.TW, q.CP, q.NCF);
   q.grid = (int)std::max<long>(1, std::min<long>(q.ntiles, (long)occ * conv_cu_count()));
   *g = q;
   return true;
@@ -912,8 +917,10 @@ static void launch_direct_epi(const DirectParams& p, int mode, int epi, int grid
     if (epi == EPI_STATS) launch_direct<T, TW, CP, NCF, MODE_FWD, EPI_STATS>(p, grid, st);
     else launch_direct<T, TW, CP, NCF, MODE_FWD, EPI_AFFINE>(p, grid, st);
   } else if (p.bws) {
-    if (epi == EPI_ACCUM) launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_ACCUM, true>(p, grid, st);
-    else launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_STORE, true>(p, grid, st);
+    if constexpr (NCF == 1) {     // (conv_direct_geometry admits the BN-reduce epilogue on NCF = 1 only)
+      if (epi == EPI_ACCUM) launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_ACCUM, true>(p, grid, st);
+      else launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_STORE, true>(p, grid, st);
+    }
   } else {
     if (epi == EPI_ACCUM) launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_ACCUM>(p, grid, st);
     else launch_direct<T, TW, CP, NCF, MODE_DGRAD, EPI_STORE>(p, grid, st);
@@ -935,8 +942,10 @@ static void launch_dgrad2_k(const DirectParams& p, int grid, hipStream_t st) {
 template <typename T, int TW, int CP, int NCF>
 static void launch_dgrad2(const DirectParams& p, int epi, int grid, hipStream_t st) {
   if (p.bws) {
-    if (epi == EPI_ACCUM) launch_dgrad2_k<T, TW, CP, NCF, EPI_ACCUM, true>(p, grid, st);
-    else launch_dgrad2_k<T, TW, CP, NCF, EPI_STORE, true>(p, grid, st);
+    if constexpr (NCF == 1) {
+      if (epi == EPI_ACCUM) launch_dgrad2_k<T, TW, CP, NCF, EPI_ACCUM, true>(p, grid, st);
+      else launch_dgrad2_k<T, TW, CP, NCF, EPI_STORE, true>(p, grid, st);
+    }
   } else {
     if (epi == EPI_ACCUM) launch_dgrad2_k<T, TW, CP, NCF, EPI_ACCUM, false>(p, grid, st);
     else launch_dgrad2_k<T, TW, CP, NCF, EPI_STORE, false>(p, grid, st);

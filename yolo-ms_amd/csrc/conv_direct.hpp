@@ -20,7 +20,9 @@ struct DirectGeo {
 // mode 0 = stride-1 forward (reduction = cin), 1 = input gradient (reduction = cout) of a stride-1
 // conv, or of a stride-2 conv by output parity class (grid width ceil(w / 2) a multiple of 16).
 // Off when YMS_DIRECT=0 at the first call or after yms_conv_direct_set(0) (A/B and tests).
-bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g);
+// bnred: the input gradient with the producer's BN-reduce epilogue (yms_conv_dgrad_bnred): <= 32
+// dx channels, one block per CU (its grid = the partial-row count).
+bool conv_direct_geometry(const yms_conv_shape* s, int mode, DirectGeo* g, bool bnred = false);
 
 // The producer's BN + act backward reduce fused into an input gradient's epilogue (yms_conv_dgrad_bnred):
 // z view of the dx pixels, its BN scale / shift / [mean | invstd], act, partial rows ws[grid][2][cin].

@@ -1619,7 +1619,7 @@ yms_status yms_conv_dgrad(const yms_conv_shape* s, const void* dz, int dz_ld, in
 
 int yms_conv_dgrad_bnred_rows(const yms_conv_shape* s) {
   DirectGeo dg;
-  if (!shape_ok(s) || s->cin % 8 != 0 || !conv_direct_geometry(s, 1, &dg)) return 0;
+  if (!shape_ok(s) || s->cin % 8 != 0 || !conv_direct_geometry(s, 1, &dg, true)) return 0;
   return dg.grid;
 }
 
@@ -1633,7 +1633,7 @@ yms_status yms_conv_dgrad_bnred(const yms_conv_shape* s, const void* dz, int dz_
     return YMS_ERR_INVALID;
   if (act != YMS_ACT_NONE && act != YMS_ACT_SILU) return YMS_ERR_INVALID;
   DirectGeo dg;
-  if (s->cin % 8 != 0 || !conv_direct_geometry(s, 1, &dg)) return YMS_ERR_UNSUPPORTED;
+  if (s->cin % 8 != 0 || !conv_direct_geometry(s, 1, &dg, true)) return YMS_ERR_UNSUPPORTED;
   const DirectBnRed b{z, z_ld, z_off, scale, shift, mean_invstd, act, ws};
   return conv_direct_launch(s, 1, dg, dz, dz_ld, dz_off, wpacked_t, dx, dx_ld, dx_off, nullptr, nullptr, 0, nullptr,
                             0, 0, nullptr, accumulate, (hipStream_t)stream, &b);
