@@ -36,3 +36,10 @@ for qid, ks in sorted(q.items(), key=lambda kv: -len(kv[1])):
     for s, e, n in ks:
         if e >= t1 - tail * 1e6:
             print(f"   {s / 1e6:8.3f} - {e / 1e6:8.3f}  {(e - s) / 1e3:7.1f} us  {n}")
+
+# the largest idle gaps of the busiest queue (what ran before / after)
+qid, ks = max(q.items(), key=lambda kv: len(kv[1]))
+gaps = sorted(((ks[i + 1][0] - ks[i][1], i) for i in range(len(ks) - 1)), reverse=True)[:15]
+print(f"-- queue {qid}: idle {sum(max(0, ks[i + 1][0] - ks[i][1]) for i in range(len(ks) - 1)) / 1e6:.3f} ms in gaps; largest:")
+for g, i in gaps:
+    print(f"   {g / 1e3:7.1f} us at {ks[i][1] / 1e6:8.3f} ms  after {ks[i][2]}  before {ks[i + 1][2]}")

@@ -195,6 +195,9 @@ class Rt:
         self.main = None         # backward: torch stream objects (main, weight-gradient side stream)
         self.side = None
         self.gover = None        # backward: buffer idx -> incoming output-gradient tensor used in place
+        # backward: enqueue each layer's weight gradient (side stream) BEFORE its input gradient, so
+        # the side stream's wait on the main stream ends at the BN apply, not after the dgrad
+        self.wgrad_first = os.environ.get("YMS_WGRAD_FIRST", "0") != "0"
 
     def a(self, v):
         return self.base + v.buf.off
@@ -374,7 +377,9 @@ class ConvOp:
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
                base + self.sh, base + self.mi, coef, self.act, dz, self.zld, 0, gres, gro[0], gro[1], self.acc_res,
                rt.st)
-        if x.buf.needs_grad:
+        def dgrad():
+            if not x.buf.needs_grad:
+                return
             q = self.bnred_for
             if q is not None:
                 # + the producer's BN-backward reduce in the epilogue (dx = the producer's final gy)
@@ -384,11 +389,16 @@ class ConvOp:
             else:
                 L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
                        self.acc_x, rt.st)
+
         dw = rt.pgrad(self.pw)
+        if not rt.wgrad_first:
+            dgrad()
         if dw is not None:
             wsz = self.wg_ws
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, 0,
                    rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
+        if rt.wgrad_first:
+            dgrad()
 
     def grad_params(self):
         return [self.pb, self.pg, self.pw]
@@ -531,19 +541,25 @@ class SiblingConvOp:
         dz = z                   # dz overwrites z in place
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, gy, gyl, gyo, base + self.sc,
                base + self.sh, base + self.mi, coef, self.act, dz, self.zld, 0, None, 0, 0, 0, rt.st)
-        if x.buf.needs_grad:
-            L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
-                   self.acc_x, rt.st)
+        def dgrad():
+            if x.buf.needs_grad:
+                L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                       self.acc_x, rt.st)
+
+        if not rt.wgrad_first:
+            dgrad()
         dw = self._adjacent(rt, "pw")
         if dw is not None:
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, 0,
                    rt.gbase + rt.plan.gscratch["wgrad"], self.wg_ws, dw, 0, rt.wst())
-            return
-        for m, off in zip(self.members, self.offs):
-            d = rt.pgrad(m.pw)
-            if d is not None:
-                L.call("yms_conv_wgrad", m.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, off,
-                       rt.gbase + rt.plan.gscratch["wgrad"], m.wg_ws, d, 0, rt.wst())
+        else:
+            for m, off in zip(self.members, self.offs):
+                d = rt.pgrad(m.pw)
+                if d is not None:
+                    L.call("yms_conv_wgrad", m.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, off,
+                           rt.gbase + rt.plan.gscratch["wgrad"], m.wg_ws, d, 0, rt.wst())
+        if rt.wgrad_first:
+            dgrad()
 
     def grad_params(self):
         # member-major within each kind: the flat arena then holds [dbeta_a | dbeta_b],
@@ -611,13 +627,19 @@ class BiasConvOp:
         if db is not None:
             L.call("yms_bias_bwd", rt.plan.dt, self.npix, self.c, gy, gyl, gyo,
                    rt.gbase + rt.plan.gscratch["bwd"], rt.cnt(self.cnt), db, rt.st)
-        if x.buf.needs_grad:
-            L.call("yms_conv_dgrad", self.sp, gy, gyl, gyo, rt.base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
-                   self.acc_x, rt.st)
+        def dgrad():
+            if x.buf.needs_grad:
+                L.call("yms_conv_dgrad", self.sp, gy, gyl, gyo, rt.base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
+                       self.acc_x, rt.st)
+
+        if not rt.wgrad_first:
+            dgrad()
         dw = rt.pgrad(self.pw)
         if dw is not None:
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, gy, gyl, gyo,
                    rt.gbase + rt.plan.gscratch["wgrad"], self.wg_ws, dw, 0, rt.wst())
+        if rt.wgrad_first:
+            dgrad()
 
     def grad_params(self):
         return [self.pbias, self.pw]
@@ -712,13 +734,15 @@ class DWConvOp(ConvOp):
         L.call("yms_bn_act_bwd_apply", dt, self.npix, c, z, self.zld, 0, rt.g(y), y.buf.ld, y.off, base + self.sc,
                base + self.sh, base + self.mi, coef, self.act, z, self.zld, 0, None, 0, 0, 0, rt.st)
         w = self.mod.conv.weight.data_ptr()
-        if x.buf.needs_grad:
+        if x.buf.needs_grad and not rt.wgrad_first:
             L.call("yms_dwconv_dgrad", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
         dw = rt.pgrad(self.pw)
         if dw is not None:
             wsz = self.wg_ws
             L.call("yms_dwconv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, z, self.zld, 0,
                    rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
+        if x.buf.needs_grad and rt.wgrad_first:
+            L.call("yms_dwconv_dgrad", self.sp, z, self.zld, 0, w, rt.g(x), x.buf.ld, x.off, self.acc_x, rt.st)
 
 
 class AddOp:
