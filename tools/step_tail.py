@@ -43,3 +43,11 @@ gaps = sorted(((ks[i + 1][0] - ks[i][1], i) for i in range(len(ks) - 1)), revers
 print(f"-- queue {qid}: idle {sum(max(0, ks[i + 1][0] - ks[i][1]) for i in range(len(ks) - 1)) / 1e6:.3f} ms in gaps; largest:")
 for g, i in gaps:
     print(f"   {g / 1e3:7.1f} us at {ks[i][1] / 1e6:8.3f} ms  after {ks[i][2]}  before {ks[i + 1][2]}")
+
+# every kernel of the busiest queue in a window [a, b] ms (argv 3, 4)
+if len(sys.argv) > 4:
+    a, b = float(sys.argv[3]) * 1e6, float(sys.argv[4]) * 1e6
+    print(f"-- queue {qid}, kernels in [{sys.argv[3]}, {sys.argv[4]}] ms")
+    for s, e, n in ks:
+        if e >= a and s <= b:
+            print(f"   {s / 1e6:8.3f} - {e / 1e6:8.3f}  {(e - s) / 1e3:7.1f} us  {n}")
