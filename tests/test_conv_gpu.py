@@ -235,11 +235,13 @@ def test_conv3x3_s1_default_paths(shp):
 # halo-tiled 3x3 weight gradient (wgrad_halo.hip): patch widths TW = W (W <= 40), divisors of W,
 # W not a multiple of TW; stride 1 / 2 with odd sizes (halo clipping at every border); cout of one
 # or two 32-blocks with padding (16, 48, 80, 130); cin not a multiple of 32 (8, 40, 96); many
-# patches per split (n = 6); images spanning patch rows.
+# patches per split (n = 6); images spanning patch rows; the 64-input-channel block variant.
 WGH = [
     (2, 32, 20, 20, 32, 1), (3, 40, 13, 27, 48, 1), (2, 64, 80, 80, 64, 1), (1, 96, 50, 70, 80, 1),
     (2, 8, 33, 41, 16, 2), (2, 64, 40, 40, 130, 2), (1, 32, 161, 97, 64, 2), (6, 64, 24, 24, 64, 1),
     (1, 16, 7, 300, 32, 1), (2, 48, 9, 5, 40, 2),
+    # one block over all 64 input channels (4 x 16 patches): ragged patch rows, padded input channels
+    (3, 64, 21, 32, 64, 1), (1, 60, 18, 48, 64, 1),
 ]
 
 

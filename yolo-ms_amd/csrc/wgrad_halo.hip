@@ -253,6 +253,17 @@ bool wgrad_halo_plan(const yms_conv_shape* s, WHPlan* w) {
   q.kp = q.S == 1 ? 128 : 64;
   q.hb = q.S == 1 ? 256 : 384;
   q.TW = std::min(pick_tw(s->wo), q.kp);
+  // 64 -> 64 stride-1 layers (the 80^2 C2f bottlenecks): with 32-channel input blocks every dz
+  // patch is read twice, once per block (PMC: 2.44x the algorithmic bytes on the YOLOv8-s step's
+  // seven such layers, profiles/r06_wgrad_pmc_layers.txt); one block covering all 64 input
+  // channels (12 waves) reads dz once, on 64-pixel patches of 4 x 16 (halo 6 x 18 = 1.69x)
+  if (q.S == 1 && q.mb == 2 && rup(s->cin, 8) == 64 && s->wo % 16 == 0 && s->ho >= 4 &&
+      env_int_wh("YMS_WG_HALO_NB2", 1)) {
+    q.nb = 2;
+    q.kp = 64;
+    q.hb = 128;
+    q.TW = 16;
+  }
   q.R = std::max(1, std::min(s->ho, q.kp / q.TW));
   for (;;) {
     q.HR = (q.R - 1) * q.S + 3;
@@ -296,6 +307,7 @@ template <typename T>
 static void dispatch_wh(const WHPlan& w, const WHParams& p, int blocks, hipStream_t st) {
   if (w.S == 1) {
     if (w.mb == 1) launch_wh<T, 1, 1, 1, 2, 128, 256, 2>(p, blocks, st);
+    else if (w.nb == 2) launch_wh<T, 1, 2, 2, 1, 64, 128, 2>(p, blocks, st);
     else launch_wh<T, 1, 2, 1, 1, 128, 256, 2>(p, blocks, st);
   } else {
     if (w.mb == 1) launch_wh<T, 2, 1, 1, 2, 64, 384, 2>(p, blocks, st);
