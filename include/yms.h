@@ -312,6 +312,11 @@ yms_status yms_det_loss(int dtype, int batch, int nc, int nlevels, const void* c
                         const int* hs, const int* ws_, const float* strides, int ld, const float* targets,
                         int n_targets, float img_w, float img_h, int iou_type, const float* pos_weight,
                         const float* lambdas, void* ws, size_t ws_bytes, float* out, void* stream);
+/* bufs[i] (device, dtype, counts[i] elements; 1 <= nbuf <= 4) *= g (device fp32 scalar), in place:
+ * the loss's map gradients times the incoming d(out)/d(total) at backward time (replaces
+ * `grad * g.to(grad.dtype)` in yolov8/tools/loss.py's autograd backward; a no-op when g == 1). */
+yms_status yms_scale_by_device_scalar(int dtype, int nbuf, void* const* bufs, const long* counts, const float* g,
+                                      void* stream);
 
 /* ---- head decode + NMS ------------------------------------------------------------------- */
 /* Raw head maps lvl[i]: NHWC [n, h_i, w_i, no_ld] with channels (64 DFL box logits, nc cls

@@ -152,6 +152,27 @@ def test_loss_terms_are_reported_not_differentiable():
     assert all(p.grad is not None and torch.isfinite(p.grad).all() for p in preds)
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16, torch.float16])
+@pytest.mark.parametrize("gscale", [1.0, 2.5, 0.3, 0.0])
+def test_loss_backward_scales_by_incoming_grad(dtype, gscale):
+    """The loss's autograd backward multiplies its map gradients by the incoming d(out)/d(total) on
+    the device (yms_scale_by_device_scalar; a no-op launch for the 1.0 seed): bit-identical to
+    torch's `grad * g.to(grad.dtype)` on the g = 1 gradients, padding channels included."""
+    B, nc = 2, 7                                      # 64 + 7 = 71 channels: NHWC ld 72 (a padding lane)
+    maps = _maps(B, nc, [(8, 8), (4, 4), (2, 2)], 11)
+    tg = _targets(B, nc, 4, 12).to(DEV)
+    crit = ComputeLoss(None, nc, DEV, (64, 64))
+    ref_preds = [_channels_last(p, dtype).requires_grad_(True) for p in maps]
+    crit.loss_tensor(ref_preds, tg)[0].backward()
+    preds = [_channels_last(p, dtype).requires_grad_(True) for p in maps]
+    total = crit.loss_tensor(preds, tg)[0]
+    (total * gscale).backward()
+    g = torch.tensor(gscale, device=DEV)
+    for p, r in zip(preds, ref_preds):
+        want = r.grad * g.to(dtype)
+        assert p.grad.dtype == dtype and torch.equal(p.grad, want)
+
+
 @pytest.mark.parametrize("name", [c for c in CASES if c != "posw"])
 def test_simplified_loss_dropin_vs_reference_fixtures(name):
     """yolov8.tools.simplified_loss.SimplifiedYOLOLoss built with train.py:321-330's exact keyword set

@@ -19,6 +19,7 @@
 //
 // Reductions are deterministic (fixed-order block partials, fp64 finals).  HBM-bound: the head
 // maps are read twice (cls + box) and the gradient written once.
+#include <algorithm>
 #include <cmath>
 
 #include "yms_common.hpp"
@@ -619,6 +620,26 @@ static LossWs loss_ws(int B, int A, int nc, int M) {
   return w;
 }
 
+// d(total)/d(maps) times the incoming loss gradient g (a device scalar), in place.  The fused loss
+// writes its map gradients in the forward, before g exists; in the training loop g is the 1.0 seed
+// of loss.backward(), so every block reads g and leaves at once -- one short launch instead of an
+// elementwise pass over the 155 MB of head gradients (configs[2]).  Otherwise v = T(float(v) *
+// float(T(g))): torch's `grad * g.to(grad.dtype)`.
+struct ScaleBufs {
+  void* p[4];
+  long n[4];
+};
+
+template <typename T>
+__global__ __launch_bounds__(256) void scale_by_dev_kernel(ScaleBufs b, const float* g) {
+  const float gv = *g;
+  if (gv == 1.0f) return;
+  const float s = to_f(from_f<T>(gv));
+  T* p = (T*)b.p[blockIdx.y];
+  const long n = b.n[blockIdx.y];
+  for (long i = blockIdx.x * 256L + threadIdx.x; i < n; i += (long)gridDim.x * 256) p[i] = from_f<T>(to_f(p[i]) * s);
+}
+
 }  // namespace yms
 
 using namespace yms;
@@ -699,6 +720,27 @@ yms_status yms_det_loss(int dtype, int batch, int nc, int nlevels, const void* c
     default: return YMS_ERR_INVALID;
   }
 #undef YMS_LOSS_CASE
+  return launch_status();
+}
+
+yms_status yms_scale_by_device_scalar(int dtype, int nbuf, void* const* bufs, const long* counts, const float* g,
+                                      void* stream) {
+  if (nbuf < 1 || nbuf > 4 || !bufs || !counts || !g) return YMS_ERR_INVALID;
+  ScaleBufs b{};
+  long mx = 0;
+  for (int i = 0; i < nbuf; ++i) {
+    if (!bufs[i] || counts[i] < 0) return YMS_ERR_INVALID;
+    b.p[i] = bufs[i];
+    b.n[i] = counts[i];
+    mx = std::max(mx, counts[i]);
+  }
+  const dim3 grid((unsigned)std::max<long>(1, std::min<long>(1024, cdiv(mx, 256))), (unsigned)nbuf);
+  switch (dtype) {
+    case YMS_F32: hipLaunchKernelGGL(scale_by_dev_kernel<float>, grid, dim3(256), 0, (hipStream_t)stream, b, g); break;
+    case YMS_BF16: hipLaunchKernelGGL(scale_by_dev_kernel<bf16>, grid, dim3(256), 0, (hipStream_t)stream, b, g); break;
+    case YMS_F16: hipLaunchKernelGGL(scale_by_dev_kernel<f16>, grid, dim3(256), 0, (hipStream_t)stream, b, g); break;
+    default: return YMS_ERR_INVALID;
+  }
   return launch_status();
 }
 

@@ -111,6 +111,7 @@ _SIGS = {
     "yms_augment_image_bytes": (_SZ, []),
     "yms_augment_normalize": (_I, [_I, _I, _P, _I, _I, _P, _P, _P, _P]),
     "yms_det_loss": (_I, [_I, _I, _I, _I, _P, _P, _P, _P, _P, _I, _P, _I, _F, _F, _I, _P, _P, _P, _SZ, _P, _P]),
+    "yms_scale_by_device_scalar": (_I, [_I, _I, _P, _P, _P, _P]),
     "yms_head_decode": (_I, [_I, _I, _I, _I, _P, _P, _P, _I, _P, _P, _F, _P, _P, _P, _P]),
     "yms_dfl": (_I, [_I, _I, _I, _I, _P, _P, _P]),
     "yms_nms_prep": (_I, [_I, _I, _I, _P, _F, _P, _P, _P, _P]),

@@ -197,7 +197,10 @@ class Rt:
         self.gover = None        # backward: buffer idx -> incoming output-gradient tensor used in place
         # backward: enqueue each layer's weight gradient (side stream) BEFORE its input gradient, so
         # the side stream's wait on the main stream ends at the BN apply, not after the dgrad
-        self.wgrad_first = os.environ.get("YMS_WGRAD_FIRST", "0") != "0"
+        # (YMS_WGRAD_FIRST=1: every layer; default "tail": only the layers whose input is the stem's
+        # output, the step's tail, where the main stream has nothing left but the stem's input-side
+        # chain and the side stream's last weight gradient otherwise starts after it; 0: none)
+        self.wgrad_first = os.environ.get("YMS_WGRAD_FIRST", "tail") == "1"
 
     def a(self, v):
         return self.base + v.buf.off
@@ -248,6 +251,7 @@ class ConvOp:
         self.pb = b.param(mod.bn, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
+        self.tail_wgrad_first = False   # enqueue the weight gradient before the input gradient (Plan)
         self.bnred_for = None    # producer whose BN-backward reduce this conv's input gradient computes
         self.bnred_by = None     # consumer whose input gradient computes this conv's BN-backward reduce
         self.bnred_key = None    # grad-scratch region of those partial rows
@@ -391,13 +395,14 @@ class ConvOp:
                        self.acc_x, rt.st)
 
         dw = rt.pgrad(self.pw)
-        if not rt.wgrad_first:
+        first = rt.wgrad_first or self.tail_wgrad_first
+        if not first:
             dgrad()
         if dw is not None:
             wsz = self.wg_ws
             L.call("yms_conv_wgrad", self.sp, rt.a(x), x.buf.ld, x.off, dz, self.zld, 0,
                    rt.gbase + rt.plan.gscratch["wgrad"], wsz, dw, 0, rt.wst())
-        if rt.wgrad_first:
+        if first:
             dgrad()
 
     def grad_params(self):
@@ -583,6 +588,7 @@ class BiasConvOp:
         self.pbias = b.param(conv, "bias")
         self.flops = 2 * self.npix * self.c * conv.in_channels * k * k
         self.stem_input = None   # plan input index when this conv reads the NCHW input directly
+        self.tail_wgrad_first = False   # enqueue the weight gradient before the input gradient (Plan)
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -939,9 +945,20 @@ class Plan:
         self.scratch_req = {}
         self.n_counters = 0
         self.stem_inputs = self._find_stems()
+        if self.training and os.environ.get("YMS_WGRAD_FIRST", "tail") == "tail":
+            stem_out = {op.y.buf.idx for op in self.stem_inputs.values()}
+            for op in self.ops:
+                if type(op) is ConvOp and op.x.buf.idx in stem_out:
+                    op.tail_wgrad_first = True
         self._find_bnred()
         La, Le = Layout(), Layout()
+        # an input the stem conv reads as NCHW fp32 has no NHWC buffer: no arena bytes, and no
+        # per-step zeroing of its padding channels (3 -> 8: 419 MB, 51 us per configs[2] step)
+        stem_bufs = {self.inputs[i].buf.idx for i in self.stem_inputs}
         for buf in self.bufs:
+            if buf.idx in stem_bufs:
+                buf.off, buf.zero = 0, False
+                continue
             buf.off = La.alloc(buf.npix * buf.ld * self.es)
         self.act_bytes = La.size
         for op in self.ops:

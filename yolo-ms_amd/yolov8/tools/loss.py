@@ -78,6 +78,13 @@ def _nhwc(p):
     return base, ld
 
 
+def _storage_elems(g):
+    """Elements of the NHWC buffer under a channels-last gradient view (its padding channels, zero,
+    scale to zero)."""
+    B, C, H, W = g.shape
+    return B * H * W * g.stride(2) // W if g.stride(1) == 1 else g.numel()
+
+
 def det_loss(preds, targets, nc, img_size, strides=(8.0, 16.0, 32.0), iou_type="ciou", pos_weight=None,
              lambdas=(7.5, 0.5, 1.5), need_grad=True):
     """-> (out [4] fp32 device tensor = total, box, cls, dfl; list of gradient maps shaped like
@@ -151,7 +158,14 @@ class _DetLossFn(torch.autograd.Function):
         ctx.grads = None
         if grads is None:
             return (None, None) + (None,) * ctx.n_preds
-        return (None, None, *[gr * g.to(gr.dtype) for gr in grads])
+        # grads *= g in place on the device (a no-op launch for the 1.0 seed of loss.backward()):
+        # no elementwise pass over the head gradients, no host sync to test g
+        gf = g.detach().to(torch.float32).contiguous()
+        n = len(grads)
+        L.call("yms_scale_by_device_scalar", L.dtype_code(grads[0].dtype), n,
+               (ctypes.c_void_p * n)(*[gr.data_ptr() for gr in grads]),
+               (ctypes.c_long * n)(*[_storage_elems(gr) for gr in grads]), gf.data_ptr(), L.stream_ptr(gf.device))
+        return (None, None, *grads)
 
 
 class ComputeLoss(nn.Module):
