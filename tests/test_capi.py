@@ -122,6 +122,31 @@ def test_sibling_head_convs_plan(monkeypatch):
     assert p2.flops == p.flops and len(p2.param_refs) == len(p.param_refs)
 
 
+def test_stem_input_and_tail_wgrad_order_plan(monkeypatch):
+    """16-bit training plan: the input the stem conv reads as NCHW has no arena bytes and no zeroing
+    (its 3 -> 8 channel padding was zeroed every step), and only the conv reading the stem's output
+    enqueues its weight gradient before its input gradient (YMS_WGRAD_FIRST: 'tail' default, 0 none)."""
+    from yms import runner
+    from yms.plan import ConvOp
+    from yolov8.yolov8 import YOLOv8
+    m = YOLOv8("s", 80)
+    m.train(True)
+    x = torch.empty(4, 3, 128, 128, device="meta")
+    p = runner.get_plan(m, [x], torch.bfloat16, True)
+    (stem,) = p.stem_inputs.values()
+    ib = p.inputs[0].buf
+    assert stem is p.ops[0] and not ib.zero and all(off != ib.off or nb == 0 for off, nb in p.zero_ranges)
+    tail = [op for op in p.ops if getattr(op, "tail_wgrad_first", False)]
+    assert len(tail) == 1 and type(tail[0]) is ConvOp and tail[0].x.buf is stem.y.buf
+    p32 = runner.get_plan(m, [x], torch.float32, True)    # fp32: generic input pack, no stem kernel
+    assert not p32.stem_inputs and p32.inputs[0].buf.zero
+    monkeypatch.setenv("YMS_WGRAD_FIRST", "0")
+    m2 = YOLOv8("s", 80)
+    m2.train(True)
+    p2 = runner.get_plan(m2, [x], torch.bfloat16, True)
+    assert not any(getattr(op, "tail_wgrad_first", False) for op in p2.ops)
+
+
 def test_state_dict_keys_identical_to_reference():
     import json
     from yolov8.yolov8 import YOLOv8
