@@ -181,7 +181,6 @@ __global__ __launch_bounds__(256) void bn_finalize_small_kernel(int c, const flo
                                                                 long count, const float* g, const float* b, float* rm,
                                                                 float* rv, float momentum, float eps, float* mi,
                                                                 int mi_ld, float* scale, float* shift) {
-  prio_bn();
   __shared__ double red[FIN3_RL * 9][4];
   const int tx = threadIdx.x & 7, ty = threadIdx.x >> 3;
   const int ch = blockIdx.x * 8 + tx;
@@ -273,7 +272,6 @@ __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const
                                                          const float* scale, const float* shift, int act,
                                                          const T* res, int res_ld, int res_off, T* y,
                                                          int y_ld, int y_off, long ppb) {
-  prio_bn();
   ChanMap m(c);
   if (!m.active) return;
   const int c0 = m.g * 8, nv = min(8, c - c0);
@@ -363,7 +361,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
                                                             const float* scale, const float* shift,
                                                             const float* mi, int act, float* ws, long ppb,
                                                             BwdFin fin = BwdFin{}) {
-  prio_bn();
   __shared__ float red[2][2048 + 64];
   ChanMap m(c);
   const int c0 = m.g * 8, nv = min(8, c - c0);
@@ -536,7 +533,6 @@ __global__ __launch_bounds__(256) void bn_bwd_reduce_kernel(long npix, int c, co
 template <int TY>
 __global__ __launch_bounds__(32 * TY) void bn_bwd_finalize_kernel(int c, const float* ws, int rows, long count,
                                                                   float* dgamma, float* dbeta, float* coef) {
-  prio_bn();
   __shared__ double red[2][TY][33];
   const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;
   const int ch = blockIdx.x * 32 + tx;
@@ -582,7 +578,6 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
                                                            const float* coef, int act, T* dz, int dz_ld,
                                                            int dz_off, T* gres, int gres_ld, int gres_off,
                                                            int gres_acc, long ppb) {
-  prio_bn();
   ChanMap m(c);
   if (!m.active) return;
   const int c0 = m.g * 8, nv = min(8, c - c0);

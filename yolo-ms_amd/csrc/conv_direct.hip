@@ -213,7 +213,6 @@ __device__ __forceinline__ void cd_chan(float& n, float& m, float& q, float nb, 
 // spill -- scratch traffic would also break the counted vmcnt waits)
 template <typename T, int TW, int CP, int NCF, int MODE, int EPI, bool BNR = false>
 __global__ __launch_bounds__(512, (BNR ? 2 : 2 * DirGeo<TW, CP, NCF>::OCC)) void conv_direct_kernel(DirectParams p) {
-  prio_conv();
   static_assert(!BNR || MODE == MODE_DGRAD, "the BN-reduce epilogue belongs to the input gradient");
   using G = DirGeo<TW, CP, NCF>;
   constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
@@ -603,7 +602,6 @@ template <int TW, int CP, int NCF> struct DirGeo2 {
 
 template <typename T, int TW, int CP, int NCF, int EPI, bool BNR = false>
 __global__ __launch_bounds__(512, (BNR ? 2 : 2 * DirGeo2<TW, CP, NCF>::OCC)) void conv_direct_dgrad2_kernel(DirectParams p) {
-  prio_conv();
   using G = DirGeo2<TW, CP, NCF>;
   constexpr int NTHR = G::NTHR, TH = G::TH, HWD = G::HWD, PITCH = G::PITCH, COP = G::COP, BUF = G::BUF;
   constexpr int ES = (int)sizeof(T);

@@ -417,7 +417,6 @@ __global__ __launch_bounds__(256, 2) void conv_nt_kernel(NTParams p) {
 constexpr int NTP_MAX_AFFINE_COLS = 512;   // wider affine outputs use conv_nt_kernel
 template <typename T, int KS, int MODE, int EPI, int BM, int BN, int WGM, int WGN, int ST, bool UNI, int OCC = 2>
 __global__ __launch_bounds__(WGM * WGN * 64, OCC) void conv_ntp_kernel(NTParams p) {
-  prio_conv();
   constexpr int NTHR = WGM * WGN * 64;
   constexpr int RPP = NTHR / NT_KCH;                       // rows per load pass (one slot)
   constexpr int SLOT = RPP * 128;                          // LDS bytes per slot

@@ -165,7 +165,6 @@ __device__ __forceinline__ Raw8<T> pack_raw8(const float (&v)[8]) {
 template <typename T, int K, int MODE, int TX = DW_TX, int G = DW_G>
 __global__ __launch_bounds__(G * 64, (G >= 7 ? 2 : DwOcc<T, K>::v))
 void dwconv_kernel(DwParams p) {
-  prio_conv();
   constexpr int CB = G * 8, NT = G * 64;
   constexpr int TY = DwTy<TX>::v, CGX = TX / DW_RX;
   constexpr int P = K / 2, HW = TX + K - 1, RB = 2 * TY + K - 1;
@@ -999,7 +998,6 @@ struct DwFm {
 
 template <typename T, int K, int NCB, int MODE>
 __global__ __launch_bounds__(256, 2) void dwconv_mfma_kernel(DwParams p, int upb) {
-  prio_conv();
   using G = DwFm<K, NCB>;
   constexpr int P = G::P, SH = G::SH, XR = G::XR, XL = G::XL, NI = G::NI;
   constexpr bool STATS = MODE == DW_FWD_STATS;
@@ -1456,7 +1454,6 @@ template <typename T>
 __global__ __launch_bounds__(256) void add_views_kernel(long items, int cg, const T* a, int a_ld, int a_off,
                                                         const T* b, int b_ld, int b_off, T* y, int y_ld, int y_off,
                                                         int accumulate) {
-  prio_bn();
   for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
     const long pix = it / cg;
     const int c = (int)(it - pix * cg) * 8;
@@ -1475,7 +1472,6 @@ template <typename T>
 __global__ __launch_bounds__(256) void add_grad2_kernel(long items, int cg, const T* g, int g_ld, int g_off, T* y1,
                                                         int ld1, int off1, int acc1, T* y2, int ld2, int off2,
                                                         int acc2) {
-  prio_bn();
   for (long it = blockIdx.x * 256l + threadIdx.x; it < items; it += (long)gridDim.x * 256) {
     const long pix = it / cg;
     const int c = (int)(it - pix * cg) * 8;

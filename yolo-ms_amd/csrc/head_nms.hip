@@ -1346,12 +1346,8 @@ constexpr size_t NMS_WG_LDS = (size_t)NMS_WG_MAX * 16 + (size_t)NMS_WG_MAX * 4 +
 
 static_assert(NMS_WG_MAX * 16 + NMS_WG_MAX * 4 >= 2 * 8192 * 8, "msort8192 scratch inside s_box / s_items / s_kept");
 
-// NWW: window of 64 * NWW members (the serial chain is one scan / bit-matrix / resolve / suppress
-// round per window, so wider windows take fewer rounds for more bit-matrix work per round)
-template <int NWW>
 __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const float* bxy, float thr_f, float tr,
                                                          int gmin, int maxc, int wg_on, NmsWs ws) {
-  constexpr int WIN = 64 * NWW;
   extern __shared__ float4 s_box[];                                   // [NMS_WG_MAX] sorted boxes
   uint64_t* s_keys = reinterpret_cast<uint64_t*>(s_box);             // [8192] keys while sorting (aliases s_box)
   uint16_t* s_items = reinterpret_cast<uint16_t*>(s_box + NMS_WG_MAX);  // [NMS_WG_MAX] cell-binned
@@ -1362,8 +1358,8 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
   __shared__ float s_red[7][16];
   __shared__ int s_wsum[16];
   __shared__ int s_bad, s_nk, s_nwk, s_cut, s_m;
-  __shared__ int s_wk[WIN], s_win[WIN];
-  __shared__ unsigned long long s_wm[WIN][NWW];
+  __shared__ int s_wk[64], s_win[64];
+  __shared__ unsigned long long s_wm[64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nbig = ws.big[0];
   for (int it = blockIdx.x; it < nbig; it += gridDim.x) {
@@ -1533,12 +1529,12 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
     __syncthreads();
     const int nwords = (n + 31) >> 5;                 // <= NMS_WG_MAX / 32 = 224 <= 4 * 64
     for (;;) {
-      // 1. window (wave 0 alone, no cross-wave scan): the first WIN alive boxes after the cursor;
+      // 1. window (wave 0 alone, no cross-wave scan): the first 64 alive boxes after the cursor;
       //    lane l holds alive word w0 + l, 64 words (2048 boxes) at a time from the cursor's word
       if (wave == 0) {
         const int lo = s_cut + 1;                     // first index still to take
         int got = 0;
-        for (int w0 = lo >> 5; w0 < nwords && got < WIN; w0 += 64) {   // wave-uniform
+        for (int w0 = lo >> 5; w0 < nwords && got < 64; w0 += 64) {   // wave-uniform
           const int w = w0 + lane;
           uint32_t v = w < nwords ? s_alive[w] : 0u;
           if (w * 32 < lo) v &= ~0u << (lo - w * 32);   // only the cursor's word is partial
@@ -1550,81 +1546,55 @@ __global__ __launch_bounds__(1024) void nms_wgrid_kernel(int A, int nc, const fl
             if (lane >= o) incl += u;
           }
           int pos = got + incl - pc;
-          while (v && pos < WIN) {
+          while (v && pos < 64) {
             const int bit = __ffs(v) - 1;
             v &= v - 1u;
             s_win[pos++] = w * 32 + bit;
           }
           got += __shfl(incl, 63);
         }
-        if (lane == 0) s_m = min(WIN, got);
+        if (lane == 0) s_m = min(64, got);
       }
       __syncthreads();
       const int m = __builtin_amdgcn_readfirstlane(s_m);
       if (m == 0) break;                              // block-uniform
-      // 2. pairwise suppression bits of the window, one ballot per row and 64-member word:
-      //    s_wm[t][q] bit l = member t (higher priority) suppresses member 64q + l > t; each lane's
-      //    own member boxes loaded once
+      // 2. pairwise suppression bits of the window, one ballot per row: s_wm[t] bit l = member t
+      //    (higher priority) suppresses member l > t; each lane's own member box loaded once
       {
-        float4 bl[NWW];
-#pragma unroll
-        for (int q = 0; q < NWW; ++q) bl[q] = s_box[s_win[64 * q + lane < m ? 64 * q + lane : 0]];
+        const float4 bl = s_box[s_win[lane < m ? lane : 0]];
         for (int t = wave; t < m; t += 16) {
           const float4 bt = s_box[s_win[t]];
-#pragma unroll
-          for (int q = 0; q < NWW; ++q) {
-            const int l = 64 * q + lane;
-            const bool hit = l > t && l < m && iou_gt_f(bt, bl[q], thr_f, false);
-            const unsigned long long row = __ballot(hit);
-            if (lane == 0) s_wm[t][q] = row;
-          }
+          const bool hit = lane > t && lane < m && iou_gt_f(bt, bl, thr_f, false);
+          const unsigned long long row = __ballot(hit);
+          if (lane == 0) s_wm[t] = row;
         }
       }
       __syncthreads();
       // 3. serial greedy on the bit rows (wave 0, scalar), visiting only the members still alive:
       //    row t clears bits above t only, so jumping to the next alive member is the same walk
       if (wave == 0) {
-        unsigned long long rowl[NWW][NWW], alive[NWW];
-#pragma unroll
-        for (int a = 0; a < NWW; ++a) {
-          const int l = 64 * a + lane;
-#pragma unroll
-          for (int q = 0; q < NWW; ++q) rowl[a][q] = (q >= a && l < m) ? s_wm[l][q] : 0ull;
-          const int ma = min(64, max(0, m - 64 * a));
-          alive[a] = ma == 64 ? ~0ull : ((1ull << ma) - 1ull);
+        const int i = lane < m ? s_win[lane] : 0;
+        const unsigned long long rowl = lane < m ? s_wm[lane] : 0ull;
+        unsigned long long alive = m == 64 ? ~0ull : ((1ull << m) - 1ull);
+        unsigned long long cur = alive;
+        while (cur) {
+          const int t = __builtin_ctzll(cur);
+          const unsigned long long rt =
+              ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(rowl >> 32), t) << 32) |
+              (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowl, t);
+          alive &= ~rt;
+          cur = alive & ~((2ull << t) - 1ull);
         }
-#pragma unroll
-        for (int a = 0; a < NWW; ++a) {
-          unsigned long long cur = alive[a];
-          while (cur) {
-            const int t = __builtin_ctzll(cur);
-#pragma unroll
-            for (int q = a; q < NWW; ++q) {
-              const unsigned long long rt =
-                  ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(rowl[a][q] >> 32), t) << 32) |
-                  (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)rowl[a][q], t);
-              alive[q] &= ~rt;
-            }
-            cur = alive[a] & ~((2ull << t) - 1ull);
-          }
-        }
+        const bool kept = (alive >> lane) & 1ull;
+        const int pos = __popcll(alive & ((1ull << lane) - 1ull));
         const int nk = s_nk;
-        int base = 0;
-#pragma unroll
-        for (int a = 0; a < NWW; ++a) {
-          const int l = 64 * a + lane;
-          const bool kept = (alive[a] >> lane) & 1ull;
-          const int pos = base + __popcll(alive[a] & ((1ull << lane) - 1ull));
-          if (kept) {
-            const int i = s_win[l];
-            s_kept[nk + pos] = (uint16_t)i;             // keep list (sorted indices) in LDS
-            s_wk[pos] = i;
-          }
-          base += __popcll(alive[a]);
+        if (kept) {
+          s_kept[nk + pos] = (uint16_t)i;               // keep list (sorted indices) in LDS
+          s_wk[pos] = i;
         }
         if (lane == 0) {
-          s_nk = nk + base;
-          s_nwk = base;
+          s_nk = nk + __popcll(alive);
+          s_nwk = __popcll(alive);
           s_cut = s_win[m - 1];
         }
       }
@@ -2074,9 +2044,7 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
                             NMS_CHUNK * 8) != hipSuccess ||
         hipFuncSetAttribute((const void*)nms_big_greedy_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)NMS_GREEDY_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void*)nms_wgrid_kernel<1>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                            (int)NMS_WG_LDS) != hipSuccess ||
-        hipFuncSetAttribute((const void*)nms_wgrid_kernel<2>, hipFuncAttributeMaxDynamicSharedMemorySize,
+        hipFuncSetAttribute((const void*)nms_wgrid_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                             (int)NMS_WG_LDS) != hipSuccess)
       return YMS_ERR_LAUNCH;
     attr_set = true;
@@ -2095,16 +2063,9 @@ yms_status yms_nms_classwise(int n, int A, int nc, const float* boxes_xyxy, cons
     //    (YMS_NMS_WGRID=0: routing only); the rest stay for the kernels below (route 3)
     const char* genv = getenv("YMS_NMS_WGRID");
     const int wg_on = (genv && atoi(genv) == 0) ? 0 : 1;
-    const char* wenv = getenv("YMS_NMS_WIN");
-    const bool win128 = wenv && atoi(wenv) == 128;
-    if (!full && (wg_on || graph)) {
-      if (win128)
-        hipLaunchKernelGGL(nms_wgrid_kernel<2>, dim3(segs), dim3(1024), NMS_WG_LDS, st, A, nc, boxes_xyxy, thr_f, tr,
-                           gmin, maxc, wg_on, w);
-      else
-        hipLaunchKernelGGL(nms_wgrid_kernel<1>, dim3(segs), dim3(1024), NMS_WG_LDS, st, A, nc, boxes_xyxy, thr_f, tr,
-                           gmin, maxc, wg_on, w);
-    }
+    if (!full && (wg_on || graph))
+      hipLaunchKernelGGL(nms_wgrid_kernel, dim3(segs), dim3(1024), NMS_WG_LDS, st, A, nc, boxes_xyxy, thr_f, tr,
+                         gmin, maxc, wg_on, w);
     // 2. graph kernels on the graph list
     if (graph && !full) {
       const unsigned gsegs = (unsigned)std::min(512, n * nc);

@@ -156,19 +156,4 @@ inline yms_status launch_status() {
   return e == hipSuccess ? YMS_OK : YMS_ERR_LAUNCH;
 }
 
-// Instruction-issue priority of the main (critical-path) stream's waves over the side stream's
-// weight-gradient waves sharing a SIMD (s_setprio; dev A/B builds via tools/ab_lib.sh).
-#ifndef YMS_PRIO_BN
-#define YMS_PRIO_BN 0
-#endif
-#ifndef YMS_PRIO_CONV
-#define YMS_PRIO_CONV 0
-#endif
-__device__ __forceinline__ void prio_bn() {
-  if constexpr (YMS_PRIO_BN > 0) __builtin_amdgcn_s_setprio(YMS_PRIO_BN);
-}
-__device__ __forceinline__ void prio_conv() {
-  if constexpr (YMS_PRIO_CONV > 0) __builtin_amdgcn_s_setprio(YMS_PRIO_CONV);
-}
-
 }  // namespace yms
