@@ -254,7 +254,8 @@ class ConvOp:
         self.tail_wgrad_first = False   # enqueue the weight gradient before the input gradient (Plan)
         self.bnred_for = None    # producer whose BN-backward reduce this conv's input gradient computes
         self.bnred_by = None     # consumer whose input gradient computes this conv's BN-backward reduce
-        self.bnred_key = None    # grad-scratch region of those partial rows
+        self.bnred_key = None    # grad-scratch region of the partial rows of THIS conv's reduce
+        self.bnred_wkey = None   # grad-scratch region this conv's input gradient writes (its producer's)
 
     def layout(self, plan, La, Le):
         es = plan.es
@@ -389,7 +390,7 @@ class ConvOp:
                 # + the producer's BN-backward reduce in the epilogue (dx = the producer's final gy)
                 L.call("yms_conv_dgrad_bnred", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
                        self.acc_x, base + q.z, q.zld, 0, base + q.sc, base + q.sh, base + q.mi, q.act,
-                       rt.gbase + rt.plan.gscratch[self.bnred_key], rt.st)
+                       rt.gbase + rt.plan.gscratch[self.bnred_wkey], rt.st)
             else:
                 L.call("yms_conv_dgrad", self.sp, dz, self.zld, 0, base + self.t_wpt, rt.g(x), x.buf.ld, x.off,
                        self.acc_x, rt.st)
@@ -676,7 +677,7 @@ class DWConvOp(ConvOp):
         self.flops = 0          # not an MFMA contraction: excluded from the conv roofline
         self.dw_flops = 2 * self.npix * c * k * k
         self.stem_input = None
-        self.bnred_for = self.bnred_by = self.bnred_key = None   # (ConvOp's fused-reduce links: unused)
+        self.bnred_for = self.bnred_by = self.bnred_key = self.bnred_wkey = None   # (ConvOp's fused-reduce links: unused)
 
     def layout(self, plan, La, Le):
         es, c = plan.es, self.c
@@ -1074,7 +1075,8 @@ class Plan:
                 continue
             key = f"bnr{n}"
             n += 1
-            c.bnred_for, c.bnred_key = q, key
+            # a conv can be both: the consumer of one pair (wkey) and the producer of the next (key)
+            c.bnred_for, c.bnred_wkey = q, key
             q.bnred_by, q.bnred_key, q.bnred_rows = c, key, rows
             self.need_scratch(key, 4 * rows * 2 * r8(x.c))
 
