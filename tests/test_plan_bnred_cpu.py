@@ -35,10 +35,26 @@ def test_pairs_have_their_own_rows_region(v):
     assert all(a[1] <= b[0] for a, b in zip(spans, spans[1:]))
 
 
-def test_chained_pairs_keep_both_regions():
+class _EveryShapeFuses:
+    """The library with every 16-bit input gradient reporting fused-reduce rows (the routing of a
+    kernel that took them all), so the plan forms chains of pairs."""
+
+    def __init__(self, real):
+        self._real = real
+
+    def __getattr__(self, name):
+        if name == "yms_conv_dgrad_bnred_rows":
+            return lambda sp: 256 if sp.contents.dtype != 0 else 0
+        return getattr(self._real, name)
+
+
+def test_chained_pairs_keep_both_regions(monkeypatch):
     """A conv that is the consumer of one pair and the producer of the next (Bottleneck cv1 -> cv2
     chains, downsample -> C2f cv1) writes its producer's rows and reads its own from different
     regions (one shared attribute sent the consumer's rows into its own producer-side region)."""
+    from yms import _lib as L
+    real = L.lib()
+    monkeypatch.setattr(L, "lib", lambda: _EveryShapeFuses(real))
     p = _plan("s")
     both = [op for op in p.ops if type(op) is ConvOp and op.bnred_for is not None and op.bnred_by is not None]
     assert both
