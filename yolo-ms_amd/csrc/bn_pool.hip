@@ -261,6 +261,10 @@ constexpr int BN_UR = 4, BN_UA = 4;
 // pass reversed (after the conv that wrote z) 18.22 -> 18.17 ms; also reversing the backward
 // reduce or apply gave no more.
 constexpr bool BN_REV_AFFINE = true, BN_REV_RED = false, BN_REV_APPLY = false;
+// Non-temporal loads where a pass reads a tensor for the last time while the weight gradients run
+// beside it (the backward apply's gy and z, the forward affine's z; the reduce's reads stay cached:
+// the apply re-reads the same bytes next).  Interleaved A/B (profiles/r06s_bn_nt_ab.txt): YOLOv8-s
+// 17.72 -> 17.64 ms/step, YOLO-MS-S 35.56 -> 35.38 ms (each alone gives part of it).
 template <bool REV> __device__ __forceinline__ long block_range() {
   return REV ? (long)(gridDim.x - 1 - blockIdx.x) : (long)blockIdx.x;
 }
@@ -298,7 +302,7 @@ __global__ __launch_bounds__(256) void affine_act_kernel(long npix, int c, const
 #pragma unroll
       for (int u = 0; u < BN_U; ++u) {
         const long pix = min(b + (long)u * m.PY, p1 - 1);
-        load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
+        load_raw8_nt(z + pix * z_ld + z_off + c0, zz[u]);       // z's last read until the backward
         if (res) load_raw8(res + pix * res_ld + res_off + c0, 8, rres[u]);
       }
     };
@@ -628,8 +632,8 @@ __global__ __launch_bounds__(256) void bn_bwd_apply_kernel(long npix, int c, con
 #pragma unroll
       for (int u = 0; u < BN_UA; ++u) {
         const long pix = min(b + (long)u * m.PY, p1 - 1);
-        load_raw8(gy + pix * gy_ld + gy_off + c0, 8, g[u]);
-        load_raw8(z + pix * z_ld + z_off + c0, 8, zz[u]);
+        load_raw8_nt(gy + pix * gy_ld + gy_off + c0, g[u]);     // the last reads of gy and z
+        load_raw8_nt(z + pix * z_ld + z_off + c0, zz[u]);
         if (racc) load_raw8(gres + pix * gres_ld + gres_off + c0, 8, rres[u]);
       }
     };

@@ -111,6 +111,14 @@ __device__ __forceinline__ void load_raw8(const T* p, int valid, Raw8<T>& r) {
     __builtin_memcpy(&r, t, sizeof(t));
   }
 }
+// the same 16-B chunk(s) with the non-temporal hint: the last read of a streamed tensor, so its
+// lines do not displace ones the concurrent kernels still reuse from L2 / the Infinity Cache
+template <typename T>
+__device__ __forceinline__ void load_raw8_nt(const T* p, Raw8<T>& r) {
+#pragma unroll
+  for (int k = 0; k < (int)(sizeof(T) / 2); ++k)
+    r.v[k] = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(p) + k);
+}
 template <typename T>
 __device__ __forceinline__ void unpack8(const Raw8<T>& r, float (&f)[8]) {
   T t[8];
