@@ -1449,7 +1449,9 @@ static int dw_wgrad_blocks(const yms_dw_shape* s) {
   } while (0)
 
 // y (+)= a + b over npix x c (b may be NULL): the MS-Block branch sum (X_i + Y_{i-1}) and, with
-// b = NULL, its backward (each addend's gradient (+)= the sum's gradient); grid-stride over 16-B items
+// b = NULL, its backward (each addend's gradient (+)= the sum's gradient); grid-stride over 16-B items.
+// The 16-bit loads of a / b here and of g in add_grad2 are the tensors' last reads and carry the
+// non-temporal hint (YOLO-MS-S 34.22 -> 34.06 ms/step interleaved, profiles/r06w_add_nt_ab.txt).
 template <typename T>
 __global__ __launch_bounds__(256) void add_views_kernel(long items, int cg, const T* a, int a_ld, int a_off,
                                                         const T* b, int b_ld, int b_off, T* y, int y_ld, int y_off,
@@ -1458,8 +1460,15 @@ __global__ __launch_bounds__(256) void add_views_kernel(long items, int cg, cons
     const long pix = it / cg;
     const int c = (int)(it - pix * cg) * 8;
     float va[8], vb[8], vy[8];
-    Vec8<T>::load(a + pix * a_ld + a_off + c, va);
-    if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb);
+    if constexpr (sizeof(T) == 2) {         // the addends' last reads: non-temporal
+      Raw8<T> ra, rb;
+      load_raw8_nt(a + pix * a_ld + a_off + c, ra);
+      unpack8(ra, va);
+      if (b) { load_raw8_nt(b + pix * b_ld + b_off + c, rb); unpack8(rb, vb); }
+    } else {
+      Vec8<T>::load(a + pix * a_ld + a_off + c, va);
+      if (b) Vec8<T>::load(b + pix * b_ld + b_off + c, vb);
+    }
     if (accumulate) Vec8<T>::load(y + pix * y_ld + y_off + c, vy);
 #pragma unroll
     for (int k = 0; k < 8; ++k) va[k] = (b ? va[k] + vb[k] : va[k]) + (accumulate ? vy[k] : 0.0f);
@@ -1476,7 +1485,13 @@ __global__ __launch_bounds__(256) void add_grad2_kernel(long items, int cg, cons
     const long pix = it / cg;
     const int c = (int)(it - pix * cg) * 8;
     float vg[8], v1[8], v2[8];
-    Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
+    if constexpr (sizeof(T) == 2) {         // the sum gradient's last read: non-temporal
+      Raw8<T> rg;
+      load_raw8_nt(g + pix * g_ld + g_off + c, rg);
+      unpack8(rg, vg);
+    } else {
+      Vec8<T>::load(g + pix * g_ld + g_off + c, vg);
+    }
     if (acc1) Vec8<T>::load(y1 + pix * ld1 + off1 + c, v1);
     if (acc2) Vec8<T>::load(y2 + pix * ld2 + off2 + c, v2);
 #pragma unroll
